@@ -1,0 +1,126 @@
+"""Python face of the native `aln` engine, mirroring the reference C++ API.
+
+    Aligner().execute(["aln", "-i", q, "-d", db, "-o", out, ...])
+        reference Aligner::Execute (aligner.cpp:65-223) — same flags, same output.
+
+    Session(argv)            inputs loaded once and resident in HBM; .run() is the
+                             hot path (seed -> score -> merge -> traceback ->
+                             E-value text), repeatable, with .output(), .hits(),
+                             .stats().
+
+Everything runs in libghostm_hip.so (HIP kernels for gfx950 + host merge); this
+module only marshals arguments.
+"""
+from __future__ import annotations
+
+import ctypes
+import subprocess
+from typing import Sequence
+
+import numpy as np
+
+from . import native
+
+HIT_DTYPE = np.dtype(
+    [
+        ("query_id", "<u4"),
+        ("db_id", "<u4"),
+        ("score", "<u4"),
+        ("db_start", "<u4"),
+        ("db_end", "<u4"),
+        ("aln_len", "<u4"),
+        ("aln_match", "<u4"),
+        ("seq_id", "<f4"),
+    ]
+)
+
+
+class GhostmError(RuntimeError):
+    pass
+
+
+class Aligner:
+    """reference class Aligner (aligner.h:63-92): Execute(argc, argv)."""
+
+    def execute(self, argv: Sequence[str]) -> int:
+        lib = native.load()
+        args = list(argv)
+        return int(lib.GhostmAlignMain(len(args), native.argv_array(args)))
+
+
+class Session:
+    def __init__(self, argv: Sequence[str]):
+        lib = native.load()
+        args = ["aln"] + list(argv)
+        self._argv = native.argv_array(args)
+        self._h = lib.GhostmSessionCreate(len(args), self._argv)
+        if not self._h:
+            raise GhostmError(native.last_error())
+
+    def run(self) -> None:
+        if native.load().GhostmSessionRun(self._h) != 0:
+            raise GhostmError(native.last_error())
+
+    def output(self) -> bytes:
+        lib = native.load()
+        n = lib.GhostmSessionOutput(self._h, None, 0)
+        buf = ctypes.create_string_buffer(n)
+        lib.GhostmSessionOutput(self._h, buf, n)
+        return buf.raw[:n]
+
+    def write(self) -> None:
+        if native.load().GhostmSessionWrite(self._h) != 0:
+            raise GhostmError(native.last_error())
+
+    def hits(self) -> np.ndarray:
+        lib = native.load()
+        n = lib.GhostmSessionHits(self._h, None, 0)
+        out = np.zeros(n, dtype=HIT_DTYPE)
+        if n:
+            lib.GhostmSessionHits(self._h, out.ctypes.data_as(ctypes.POINTER(native.GhostmHit)), n)
+        return out
+
+    def stats(self) -> dict:
+        st = native.GhostmStats()
+        native.load().GhostmSessionStats(self._h, ctypes.byref(st))
+        return st.as_dict()
+
+    def close(self) -> None:
+        if self._h:
+            native.load().GhostmSessionDestroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def run_cli(args: Sequence[str], **kw) -> subprocess.CompletedProcess:
+    """Run the native `ghostm` binary (db | qry | aln | synth)."""
+    return subprocess.run([native.BIN_PATH] + list(args), check=True, capture_output=True, **kw)
+
+
+def format_db(fasta: str, prefix: str, *extra: str) -> None:
+    run_cli(["db", "-i", fasta, "-o", prefix, *extra])
+
+
+def format_queries(fasta: str, prefix: str, *extra: str) -> None:
+    run_cli(["qry", "-i", fasta, "-o", prefix, *extra])
+
+
+def synth(db_fasta: str | None, query_fasta: str | None, nq: int, db_residues: int, seed: int,
+          *extra: str) -> None:
+    args = ["synth", "-n", str(nq), "-N", str(db_residues), "-s", str(seed)]
+    if db_fasta:
+        args += ["-d", db_fasta]
+    if query_fasta:
+        args += ["-q", query_fasta]
+    run_cli(args + list(extra))

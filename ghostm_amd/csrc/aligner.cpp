@@ -1,0 +1,451 @@
+// aligner.cpp — see aligner.h.
+#include "aligner.h"
+
+#include <getopt.h>
+
+#include <algorithm>
+#include <atomic>
+#include <exception>
+#include <climits>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <stdexcept>
+#include <thread>
+
+#include "common.h"
+
+namespace ghostm {
+
+unsigned HostThreads() {
+  if (const char *e = getenv("GHOSTM_THREADS")) {
+    const int v = atoi(e);
+    if (v > 0) return (unsigned)v;
+  }
+  unsigned hw = std::thread::hardware_concurrency();
+  if (hw == 0) hw = 1;
+  return std::min(hw, 16u);
+}
+
+void ParallelFor(size_t n, unsigned threads,
+                 const std::function<void(size_t, size_t, unsigned)> &fn) {
+  if (n == 0) return;
+  threads = (unsigned)std::max<size_t>(1, std::min<size_t>(threads, n));
+  if (threads == 1) {
+    fn(0, n, 0);
+    return;
+  }
+  std::vector<std::thread> pool;
+  std::vector<std::exception_ptr> errors(threads);
+  const size_t per = (n + threads - 1) / threads;
+  for (unsigned t = 0; t < threads; ++t) {
+    const size_t b = t * per, e = std::min(n, b + per);
+    if (b >= e) break;
+    pool.emplace_back([&fn, &errors, b, e, t] {
+      try {
+        fn(b, e, t);
+      } catch (...) {
+        errors[t] = std::current_exception();
+      }
+    });
+  }
+  for (auto &th : pool) th.join();
+  for (auto &ep : errors)
+    if (ep) std::rethrow_exception(ep);
+}
+
+AlignerOptions ParseAlignerOptions(int argc, char **argv) {
+  AlignerOptions o;
+  std::string matrix_file = "BLOSUM62";
+  optind = 1;
+  opterr = 1;
+  int c;
+  while ((c = getopt(argc, argv, "b:d:D:e:E:G:i:l:M:o:r:s:t:S:L:y:v")) >= 0) {
+    switch (c) {
+      case 'b': o.best = atoi(optarg); break;
+      case 'd': o.db_prefix = optarg; break;
+      case 'D': o.device = atoi(optarg); break;
+      case 'e': o.extend = atoi(optarg); break;
+      case 'E': o.extend_gap = -atoi(optarg); break;
+      case 'G': o.open_gap = -atoi(optarg); break;
+      case 'i': o.query_prefix = optarg; break;
+      case 'S': o.start_query_chunk = atoi(optarg); break;
+      case 'L': o.end_query_chunk = atoi(optarg); break;
+      case 'l': o.max_list_length = atoi(optarg) * (1 << 20); break;
+      case 'M': matrix_file = optarg; break;
+      case 'o': o.output_file = optarg; break;
+      case 'r': {
+        const int lr = (int)log2(atoi(optarg));
+        o.log_region = lr < 1 ? 1 : lr;
+        break;
+      }
+      case 's': o.shift = atoi(optarg); break;
+      case 't': o.threshold = atoi(optarg); break;
+      case 'y': o.output_style = atoi(optarg); break;
+      case 'v': o.verbose = true; break;
+      default: throw std::invalid_argument("");
+    }
+  }
+  // test hook: -l in candidates instead of MiB units (exercises batch cuts on
+  // small inputs); the oracle honours the same variable
+  if (const char *e = getenv("GHOSTM_MAX_LIST_OVERRIDE")) o.max_list_length = (uint32_t)strtoul(e, nullptr, 10);
+  o.matrix = ReadScoreMatrix(matrix_file);
+  if (o.output_style == 0) o.karlin = GappedKarlinParams(o.matrix, o.open_gap, o.extend_gap);
+  return o;
+}
+
+// ------------------------------------------------------------------ session
+Session::Session(const AlignerOptions &opt) : opt_(opt) {
+  threads_ = HostThreads();
+  DeviceModule &dev = DeviceModule::Get();
+  dev.Bind(opt_.device);
+  dev.SetMatrix(opt_.matrix.m.data());
+
+  // query chunks: -S start (or 0) .. -L end, as Execute walks them (aligner.cpp:98-204)
+  QueryFile qf(opt_.query_prefix);
+  uint32_t id = opt_.start_query_chunk == UINT32_MAX ? 0 : opt_.start_query_chunk;
+  uint32_t base = 0;
+  for (uint32_t k = 0; k < id && k < qf.division; ++k) {
+    std::ifstream f((qf.prefix + "_" + std::to_string(k) + ".inf").c_str(), std::ios::binary);
+    uint32_t n = 0;
+    if (f) f.read(reinterpret_cast<char *>(&n), 4);
+    base += n;
+  }
+  for (;;) {
+    QueryData qd;
+    if (!qf.ReadChunk(id, &qd.chunk)) break;
+    qd.global_base = base;
+    base += qd.chunk.nseq;
+    queries_.push_back(std::move(qd));
+    ++id;
+    if (!(id <= opt_.end_query_chunk)) break;
+  }
+  if (queries_.empty()) throw std::runtime_error("[Aligner] error: don't find query file.");
+
+  DbFile df(opt_.db_prefix);
+  db_sum_u32_ = (uint32_t)df.sum_length;
+  uint32_t dbase = 0;
+  for (uint32_t k = 0;; ++k) {
+    DbData dd;
+    if (!df.ReadChunk(k, &dd.chunk)) break;
+    dd.global_base = dbase;
+    dbase += dd.chunk.nseq;
+    dbs_.push_back(std::move(dd));
+  }
+  if (dbs_.empty()) throw std::runtime_error("[Aligner] error: don't find db file.");
+
+  for (QueryData &q : queries_) {
+    const uint32_t n = q.chunk.nseq, L = q.chunk.L;
+    q.group_end.assign(n, 0);
+    for (uint32_t i = n; i-- > 0;) {
+      q.group_end[i] = (i + 1 < n && q.chunk.names[i + 1] == q.chunk.names[i]) ? q.group_end[i + 1] : i + 1;
+    }
+    q.qlen.assign(n, 1);
+    for (uint32_t i = 0; i < n; ++i) {
+      const uint8_t *s = &q.chunk.seq[(size_t)i * L];
+      uint32_t e = L - 1;
+      while (e > 0 && s[e] == kBaseX) --e;
+      q.qlen[i] = e + 1;
+    }
+    q.dev = dev.UploadQuery(q.chunk.seq.data(), n, L);
+  }
+  for (DbData &d : dbs_) {
+    const DbChunk &c = d.chunk;
+    d.dev = dev.UploadDb(c.seq.data(), c.len, c.keys_count.data(), c.kcl, c.positions.data(), c.npos);
+  }
+  dev.Synchronize();
+}
+
+Session::~Session() {
+  DeviceModule &dev = DeviceModule::Get();
+  for (QueryData &q : queries_) dev.Free(q.dev);
+  for (DbData &d : dbs_) dev.Free(d.dev);
+}
+
+// The CPU path's batch cuts (aligner.cpp:383-521 driven by Execute's loop at
+// 131-171): a query whose candidates push the running total above -l is carried
+// into the next batch; the loop stops at the first empty batch, so a carried last
+// query is dropped, exactly as the reference does.
+struct Batch {
+  uint32_t q0, q1;  // queries [q0, q1)
+};
+
+static std::vector<Batch> CpuBatches(const std::vector<uint32_t> &counts, uint64_t max_list) {
+  std::vector<Batch> out;
+  const uint32_t n = (uint32_t)counts.size();
+  uint32_t next = 0;
+  int64_t carry = -1;
+  for (;;) {
+    if (next == n) break;
+    uint32_t first = next;
+    uint64_t total = 0;
+    if (carry >= 0) {
+      first = (uint32_t)carry;
+      total = counts[carry];
+    }
+    carry = -1;
+    uint32_t i = next;
+    bool cut = false;
+    for (; i < n; ++i) {
+      total += counts[i];
+      if (total > max_list) { cut = true; break; }
+    }
+    const uint64_t cands = cut ? total - counts[i] : total;
+    const uint32_t stop = cut ? i : n;
+    if (cut) { next = i + 1; carry = i; } else { next = n; }
+    if (cands == 0) break;
+    out.push_back(Batch{first, stop});
+  }
+  return out;
+}
+
+namespace {
+struct MergeItem {
+  uint32_t score;
+  uint32_t end;       // absolute db end (new) / unused (resolved)
+  uint32_t query;     // candidate's own query (frame)
+  int32_t from;       // -1: new candidate; else position in the group's old results
+};
+struct ScoreDesc {
+  bool operator()(const MergeItem &a, const MergeItem &b) const { return a.score > b.score; }
+};
+}  // namespace
+
+// reference Merge (aligner.cpp:687-769): per name group, the batch's candidates
+// of each query then its kept results, std::sort by score (unstable), first hit
+// per subject traced back, stop at -b. Groups are independent -> host threads.
+void Session::MergeBatch(QueryData &q, DbData &d, uint32_t bq0, uint32_t bq1,
+                         uint64_t cand_begin, const uint32_t *score, const uint32_t *end,
+                         const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets,
+                         Results *results) {
+  const uint32_t n = q.chunk.nseq;
+  std::vector<uint32_t> group_starts;
+  for (uint32_t i = 0; i < n; i = q.group_end[i]) group_starts.push_back(i);
+  const uint64_t epoch = ++merge_epoch_;
+  const uint32_t nsubj = d.chunk.nseq;
+  struct Pending {
+    uint32_t id, pos;
+  };
+  std::vector<std::vector<Pending>> pending(threads_);
+  ParallelFor(group_starts.size(), threads_, [&](size_t gb, size_t ge, unsigned t) {
+    std::vector<uint64_t> owner(nsubj, ~0ull);
+    std::vector<MergeItem> l;
+    std::vector<HitRecord> old;
+    for (size_t g = gb; g < ge; ++g) {
+      const uint32_t gs = group_starts[g], gend = q.group_end[gs], id = gend - 1;
+      l.clear();
+      old.clear();
+      for (uint32_t i = gs; i < gend; ++i) {
+        if (i >= bq0 && i < bq1) {
+          const uint64_t b = offsets[i] - cand_begin;
+          for (uint32_t k = 0; k < counts[i]; ++k)
+            l.push_back(MergeItem{score[b + k], end[b + k], i, -1});
+        }
+        for (HitRecord &h : (*results)[i]) {
+          l.push_back(MergeItem{h.score, 0, h.query, (int32_t)old.size()});
+          old.push_back(h);
+        }
+        (*results)[i].clear();
+      }
+      if (l.empty()) continue;
+      std::sort(l.begin(), l.end(), ScoreDesc());
+      std::vector<HitRecord> &out = (*results)[id];
+      const uint64_t tag = (epoch << 32) | id;
+      for (const MergeItem &it : l) {
+        if (it.from >= 0) {
+          out.push_back(old[it.from]);
+        } else {
+          const uint32_t sid = d.chunk.SubjectOf(it.end);
+          if (sid >= nsubj) throw Error("candidate end outside the database");
+          if (owner[sid] != tag) {
+            owner[sid] = tag;
+            HitRecord h;
+            h.query = it.query;
+            h.db_chunk = d.chunk.id;
+            h.subject = sid;
+            h.score = it.score;
+            h.end = it.end;          // absolute until the traceback
+            h.start = UINT32_MAX;
+            pending[t].push_back(Pending{id, (uint32_t)out.size()});
+            out.push_back(h);
+          }
+        }
+        if (out.size() >= opt_.best) break;
+      }
+    }
+  });
+
+  // K3 for every newly selected hit of this batch, then rebase to the subject
+  std::vector<Pending> all;
+  for (auto &p : pending) all.insert(all.end(), p.begin(), p.end());
+  const uint32_t nh = (uint32_t)all.size();
+  if (nh == 0) return;
+  std::vector<uint32_t> qid(nh), e(nh), st(nh), len(nh), mt(nh);
+  std::vector<float> sid(nh);
+  for (uint32_t k = 0; k < nh; ++k) {
+    const HitRecord &h = (*results)[all[k].id][all[k].pos];
+    qid[k] = h.query;
+    e[k] = h.end;
+  }
+  const uint32_t tb_base = q.chunk.L + 2 * opt_.extend * 2 * (1u << opt_.log_region);
+  DeviceModule::Get().TraceBack(q.dev, d.dev, nh, qid.data(), e.data(), tb_base, opt_.open_gap,
+                                opt_.extend_gap, st.data(), len.data(), mt.data(), sid.data());
+  stats_.tracebacks += nh;
+  for (uint32_t k = 0; k < nh; ++k) {
+    HitRecord &h = (*results)[all[k].id][all[k].pos];
+    const uint32_t pos = d.chunk.starts[h.subject];
+    h.start = st[k] - pos;
+    h.end = h.end - pos;
+    h.aln_len = len[k];
+    h.aln_match = mt[k];
+    h.seq_id = sid[k];
+  }
+}
+
+void Session::RunQueryChunk(QueryData &q, Results *results) {
+  DeviceModule &dev = DeviceModule::Get();
+  SeedConfig sc;
+  sc.threshold = opt_.threshold;
+  sc.shift = opt_.shift;
+  sc.log_region = opt_.log_region;
+  GapConfig gap;
+  gap.extend = opt_.extend;
+  gap.log_region = opt_.log_region;
+  gap.open = opt_.open_gap;
+  gap.ext = opt_.extend_gap;
+  const uint32_t base = q.chunk.L + 2 * opt_.extend + 2 * (1u << opt_.log_region);
+  std::vector<uint32_t> counts;
+  std::vector<uint64_t> offsets;
+  std::vector<uint32_t> score, end;
+  for (DbData &d : dbs_) {
+    sc.seed_mask = d.chunk.seed;
+    const uint64_t total = dev.Seed(q.dev, d.dev, sc, &counts, &offsets);
+    stats_.candidates += total;
+    const std::vector<Batch> batches = CpuBatches(counts, opt_.max_list_length);
+    for (const Batch &b : batches) {
+      const uint64_t c0 = offsets[b.q0];
+      const uint64_t c1 = b.q1 < counts.size() ? offsets[b.q1] : total;
+      const uint64_t nc = c1 - c0;
+      score.resize(nc);
+      end.resize(nc);
+      dev.Score(q.dev, d.dev, c0, nc, b.q0, b.q1, counts, offsets, base, gap, score.data(), end.data());
+      const double t0 = NowSeconds();
+      MergeBatch(q, d, b.q0, b.q1, c0, score.data(), end.data(), counts, offsets, results);
+      stats_.seconds_merge += NowSeconds() - t0;
+      stats_.batches += 1;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ output
+namespace {
+inline void AppendU32(std::string *s, uint32_t v) {
+  char buf[16];
+  int n = 0;
+  do { buf[n++] = (char)('0' + v % 10); v /= 10; } while (v);
+  while (n) s->push_back(buf[--n]);
+}
+inline void AppendFloat(std::string *s, float f) {
+  char buf[48];
+  const int n = snprintf(buf, sizeof(buf), "%g", (double)f);
+  s->append(buf, n);
+}
+}  // namespace
+
+// WriteOutput / V1 / V2 (aligner.cpp:951-1012): ostream << float prints "%g".
+void Session::FormatChunk(const QueryData &q, const Results &results, std::string *text,
+                          std::vector<GhostmHit> *hits) {
+  const uint32_t n = q.chunk.nseq;
+  std::vector<std::string> parts(threads_);
+  std::vector<std::vector<GhostmHit>> hparts(threads_);
+  const EvalueCalculator ev(opt_.karlin);
+  const int style = opt_.output_style;
+  ParallelFor(n, threads_, [&](size_t b, size_t e, unsigned t) {
+    std::string &s = parts[t];
+    std::vector<GhostmHit> &hv = hparts[t];
+    for (size_t i = b; i < e; ++i) {
+      const std::string &name = q.chunk.names[i];
+      const uint64_t space = (uint64_t)q.qlen[i] * (uint64_t)db_sum_u32_;
+      for (const HitRecord &h : results[i]) {
+        const DbData &d = dbs_[h.db_chunk];
+        const std::string &sname = d.chunk.names[h.subject];
+        s.append(name);
+        s.push_back('\t');
+        s.append(sname);
+        s.push_back('\t');
+        if (style == 1) {
+          AppendU32(&s, h.score); s.push_back('\t');
+          AppendU32(&s, h.start + 1); s.push_back('\t');
+          AppendU32(&s, h.end + 1);
+        } else if (style == 2) {
+          AppendU32(&s, h.score); s.push_back('\t');
+          AppendU32(&s, h.start + 1); s.push_back('\t');
+          AppendU32(&s, h.end + 1); s.push_back('\t');
+          AppendFloat(&s, h.seq_id); s.push_back('\t');
+          AppendU32(&s, h.aln_len); s.push_back('\t');
+          AppendU32(&s, h.aln_match);
+        } else {
+          AppendFloat(&s, h.seq_id * 100); s.push_back('\t');
+          AppendU32(&s, h.aln_len); s.push_back('\t');
+          AppendU32(&s, h.aln_match); s.push_back('\t');
+          AppendU32(&s, h.start + 1); s.push_back('\t');
+          AppendU32(&s, h.end + 1); s.push_back('\t');
+          AppendFloat(&s, ev.Evalue((int)h.score, space)); s.push_back('\t');
+          AppendFloat(&s, ev.Bits((int)h.score)); s.push_back('\t');
+        }
+        s.push_back('\n');
+        GhostmHit g;
+        g.query_id = q.global_base + (uint32_t)i;
+        g.db_id = d.global_base + h.subject;
+        g.score = h.score;
+        g.db_start = h.start;
+        g.db_end = h.end;
+        g.aln_len = h.aln_len;
+        g.aln_match = h.aln_match;
+        g.seq_id = h.seq_id;
+        hv.push_back(g);
+      }
+    }
+  });
+  size_t add = 0;
+  for (auto &p : parts) add += p.size();
+  text->reserve(text->size() + add);
+  for (auto &p : parts) text->append(p);
+  for (auto &h : hparts) hits->insert(hits->end(), h.begin(), h.end());
+}
+
+void Session::Run() {
+  DeviceModule &dev = DeviceModule::Get();
+  dev.ResetTimes();
+  stats_ = GhostmStats{};
+  merge_epoch_ = 0;
+  output_.clear();
+  hits_.clear();
+  const double t0 = NowSeconds();
+  for (QueryData &q : queries_) {
+    Results results(q.chunk.nseq);
+    RunQueryChunk(q, &results);
+    const double t1 = NowSeconds();
+    FormatChunk(q, results, &output_, &hits_);
+    stats_.seconds_output += NowSeconds() - t1;
+    stats_.queries += q.chunk.nseq;
+    for (uint32_t v : q.qlen) stats_.query_residues += v;
+  }
+  stats_.seconds_total = NowSeconds() - t0;
+  const DeviceTimes &dt = dev.times();
+  stats_.seconds_seed = dt.seed;
+  stats_.seconds_score = dt.score;
+  stats_.seconds_traceback = dt.traceback;
+  stats_.score_launches = dt.score_launches;
+  stats_.seed_bytes = dt.seed_bytes;
+  stats_.hits = hits_.size();
+}
+
+void Session::WriteOutputFile() const {
+  std::ofstream out(opt_.output_file.c_str(), std::ios::binary);
+  out.write(output_.data(), (std::streamsize)output_.size());
+}
+
+}  // namespace ghostm

@@ -1,0 +1,111 @@
+// aligner.h — the `aln` driver: the reference Aligner (aligner.h:42-92,
+// aligner.cpp:65-1012) re-built around the gfx950 device module.
+//
+// Same options, same chunk loops, same batch cuts, same Merge order (libstdc++
+// std::sort), same tie rules and the same text output as the reference CPU path;
+// the seed search, score DP and traceback run on the GPU, the merge selection and
+// the output formatting run on host threads.
+#pragma once
+#include <cstdint>
+#include <functional>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/ghostm_hip.h"
+#include "device.h"
+#include "formats.h"
+#include "scoring.h"
+
+namespace ghostm {
+
+// reference AlignerOption (aligner.h:42-61), defaults of SetOption (aligner.cpp:226-243)
+struct AlignerOptions {
+  std::string output_file;
+  std::string query_prefix;
+  std::string db_prefix;
+  uint32_t start_query_chunk = UINT32_MAX;
+  uint32_t end_query_chunk = UINT32_MAX;
+  uint32_t log_region = 4;
+  uint32_t shift = 2;
+  uint32_t threshold = 2;
+  uint32_t max_list_length = 1u << 27;
+  int open_gap = -11;
+  int extend_gap = -1;
+  uint32_t extend = 2;
+  uint32_t best = 10;
+  int device = 0;            // -D; the GPU path is the only path here
+  int output_style = 0;      // -y
+  bool verbose = false;
+  ScoreMatrix matrix;
+  KarlinParams karlin;
+};
+
+// getopt "b:d:D:e:E:G:i:l:M:o:r:s:t:S:L:y:v" (aligner.cpp:248); throws
+// std::invalid_argument like the reference.
+AlignerOptions ParseAlignerOptions(int argc, char **argv);
+
+// A resolved hit: what the reference keeps in an Alignment (alignment.h:136-145).
+struct HitRecord {
+  uint32_t query = 0;        // index within its query chunk
+  uint32_t db_chunk = 0;
+  uint32_t subject = 0;      // index within its DB chunk
+  uint32_t score = 0;
+  uint32_t start = 0;        // absolute until traceback + rebase, then subject-relative
+  uint32_t end = 0;
+  uint32_t aln_len = 0;
+  uint32_t aln_match = 0;
+  float seq_id = 0.f;
+};
+
+class Session {
+ public:
+  explicit Session(const AlignerOptions &opt);
+  ~Session();
+
+  void Run();                       // whole search; replaces previous results
+  const std::string &Output() const { return output_; }
+  void WriteOutputFile() const;
+  const std::vector<GhostmHit> &Hits() const { return hits_; }
+  const GhostmStats &Stats() const { return stats_; }
+
+ private:
+  struct QueryData {
+    QueryChunk chunk;
+    DevQuery *dev = nullptr;
+    std::vector<uint32_t> group_end;   // per query: one past the last query of its name group
+    std::vector<uint32_t> qlen;        // WriteOutput's query length (last non-X + 1)
+    uint32_t global_base = 0;          // index of the chunk's first query over all chunks
+  };
+  struct DbData {
+    DbChunk chunk;
+    DevDb *dev = nullptr;
+    uint32_t global_base = 0;
+  };
+
+  using Results = std::vector<std::vector<HitRecord>>;
+  void RunQueryChunk(QueryData &q, Results *results);
+  void MergeBatch(QueryData &q, DbData &d, uint32_t bq0, uint32_t bq1, uint64_t cand_begin,
+                  const uint32_t *score, const uint32_t *end, const std::vector<uint32_t> &counts,
+                  const std::vector<uint64_t> &offsets, Results *results);
+  void FormatChunk(const QueryData &q, const Results &results, std::string *text,
+                   std::vector<GhostmHit> *hits);
+
+  AlignerOptions opt_;
+  std::vector<QueryData> queries_;
+  std::vector<DbData> dbs_;
+  uint32_t db_sum_u32_ = 0;           // DBReader::GetSumDbLength() truncates to u32
+  uint64_t merge_epoch_ = 0;
+  std::string output_;
+  std::vector<GhostmHit> hits_;
+  GhostmStats stats_{};
+  unsigned threads_ = 1;
+};
+
+// Number of host worker threads (GHOSTM_THREADS, default min(16, hardware)).
+unsigned HostThreads();
+
+// Parallel for over [0, n) in contiguous blocks.
+void ParallelFor(size_t n, unsigned threads, const std::function<void(size_t, size_t, unsigned)> &fn);
+
+}  // namespace ghostm

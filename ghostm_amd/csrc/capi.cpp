@@ -1,0 +1,99 @@
+// capi.cpp — session part of the C ABI (include/ghostm_hip.h Part 2).
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <vector>
+
+#include "../../include/ghostm_hip.h"
+#include "aligner.h"
+#include "common.h"
+
+using namespace ghostm;
+
+namespace ghostm {
+void SetLastErrorMessage(const std::string &m);
+}
+
+extern "C" {
+
+void *GhostmSessionCreate(int argc, char **argv) {
+  try {
+    AlignerOptions opt = ParseAlignerOptions(argc, argv);
+    return new Session(opt);
+  } catch (std::exception &e) {
+    SetLastErrorMessage(e.what());
+    return nullptr;
+  }
+}
+
+int GhostmSessionRun(void *s) {
+  try {
+    if (!s) throw Error("null session");
+    static_cast<Session *>(s)->Run();
+    return 0;
+  } catch (std::exception &e) {
+    SetLastErrorMessage(e.what());
+    return 1;
+  }
+}
+
+size_t GhostmSessionOutput(void *s, char *buf, size_t cap) {
+  if (!s) return 0;
+  const std::string &o = static_cast<Session *>(s)->Output();
+  if (!buf) return o.size();
+  const size_t n = std::min(cap, o.size());
+  std::memcpy(buf, o.data(), n);
+  return n;
+}
+
+int GhostmSessionWrite(void *s) {
+  try {
+    if (!s) throw Error("null session");
+    static_cast<Session *>(s)->WriteOutputFile();
+    return 0;
+  } catch (std::exception &e) {
+    SetLastErrorMessage(e.what());
+    return 1;
+  }
+}
+
+size_t GhostmSessionHits(void *s, GhostmHit *hits, size_t cap) {
+  if (!s) return 0;
+  const std::vector<GhostmHit> &h = static_cast<Session *>(s)->Hits();
+  if (!hits) return h.size();
+  const size_t n = std::min(cap, h.size());
+  std::memcpy(hits, h.data(), n * sizeof(GhostmHit));
+  return n;
+}
+
+int GhostmSessionStats(void *s, GhostmStats *stats) {
+  if (!s || !stats) return 1;
+  *stats = static_cast<Session *>(s)->Stats();
+  return 0;
+}
+
+void GhostmSessionDestroy(void *s) { delete static_cast<Session *>(s); }
+
+// `ghostm aln` (reference Aligner::Execute via main.cpp:107-121): the output file
+// is opened right after option parsing; every error is printed and 0 returned.
+int GhostmAlignMain(int argc, char **argv) {
+  try {
+    AlignerOptions opt = ParseAlignerOptions(argc, argv);
+    { std::ofstream touch(opt.output_file.c_str()); }
+    Session session(opt);
+    session.Run();
+    session.WriteOutputFile();
+    if (opt.verbose) {
+      const GhostmStats &st = session.Stats();
+      std::cout << "# queries " << st.queries << " candidates " << st.candidates << " hits "
+                << st.hits << "\n# seconds total " << st.seconds_total << " seed " << st.seconds_seed
+                << " score " << st.seconds_score << " traceback " << st.seconds_traceback
+                << " merge " << st.seconds_merge << " output " << st.seconds_output << std::endl;
+    }
+  } catch (std::exception &e) {
+    std::cerr << e.what() << std::endl;
+  }
+  return 0;
+}
+
+}  // extern "C"

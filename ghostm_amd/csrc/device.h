@@ -1,0 +1,96 @@
+// device.h — host-side interface of the gfx950 device module (device.hip).
+//
+// The module owns one HIP device per process, one stream, the score tables and
+// the resident query/DB chunks, and runs the three kernel families of the `aln`
+// hot path:
+//   K1 seed      k-mer lists -> diagonal-bin candidates   (SearchNextCpu, aligner.cpp:383-521)
+//   K2 score     Gotoh local score + end per candidate    (CalculateScoreCpu, aligner.cpp:545-685)
+//   K3 traceback reverse DP -> start, length, matches    (TraceBack, aligner.cpp:771-949)
+// Everything on the device is exact integer work; the host keeps the merge
+// (libstdc++ std::sort order) and the float E-value formatting.
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace ghostm {
+
+struct SeedConfig {
+  uint32_t seed_mask = 15;   // index seed bits (db -k 4 -> 0b1111)
+  uint32_t threshold = 2;    // aln -t
+  uint32_t shift = 2;        // aln -s
+  uint32_t log_region = 4;   // log2(aln -r)
+};
+
+struct GapConfig {
+  uint32_t extend = 2;       // aln -e
+  uint32_t log_region = 4;
+  int open = -11;            // negated -G
+  int ext = -1;              // negated -E
+};
+
+// Device-resident chunk handles (opaque to callers).
+struct DevQuery;
+struct DevDb;
+
+struct DeviceTimes {
+  double seed = 0, score = 0, traceback = 0;  // seconds of device time (HIP events)
+  uint64_t seed_bytes = 0;
+  uint64_t score_launches = 0;
+};
+
+class DeviceModule {
+ public:
+  static DeviceModule &Get();
+
+  void Bind(int device);                 // hipSetDevice + stream; idempotent
+  int device() const { return device_; }
+  void SetMatrix(const int *m32x32);     // M[db*32 + q]
+  std::string DeviceName() const;
+  size_t TotalMemory() const;
+
+  DevQuery *UploadQuery(const uint8_t *seq, uint32_t nseq, uint32_t L);
+  DevDb *UploadDb(const uint8_t *seq, uint32_t len, const uint32_t *keys_count, uint32_t kcl,
+                  const uint32_t *positions, uint32_t npos);
+  void Free(DevQuery *q);
+  void Free(DevDb *d);
+
+  // K1 over every query of q against d. On return: counts[nseq] (host) and the
+  // compact device candidate arrays (start, qid) ordered by (query, start).
+  // offsets[q] = first candidate of query q. Returns total candidates.
+  uint64_t Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg, std::vector<uint32_t> *counts,
+                std::vector<uint64_t> *offsets);
+  // Copy candidate starts [begin, begin+n) to host.
+  void CopyStarts(uint64_t begin, uint64_t n, uint32_t *out);
+
+  // K2 over candidates [cand_begin, cand_begin + n) whose queries are
+  // [q_first, q_end) with per-query counts/offsets as returned by Seed.
+  // Scores/ends land in host arrays score[n], end[n].
+  void Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n, uint32_t q_first,
+             uint32_t q_end, const std::vector<uint32_t> &counts,
+             const std::vector<uint64_t> &offsets, uint32_t base_search_length,
+             const GapConfig &gap, uint32_t *score, uint32_t *end);
+
+  // K3 on n hits (query id, absolute db end).
+  void TraceBack(DevQuery *q, DevDb *d, uint32_t n, const uint32_t *qid, const uint32_t *db_end,
+                 uint32_t base_search_length, int open, int ext, uint32_t *db_start,
+                 uint32_t *aln_len, uint32_t *aln_match, float *seq_id);
+
+  DeviceTimes &times() { return times_; }
+  void ResetTimes() { times_ = DeviceTimes(); }
+  void Synchronize();
+
+ private:
+  DeviceModule() = default;
+  int device_ = -1;
+  void *stream_ = nullptr;
+  DeviceTimes times_;
+  struct Impl;
+  Impl *impl_ = nullptr;
+  friend struct DeviceModuleAccess;
+};
+
+const char *DeviceBuildInfo();
+
+}  // namespace ghostm

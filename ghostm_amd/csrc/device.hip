@@ -1,0 +1,761 @@
+// device.hip — gfx950 device module: buffers, launches, and the reference C ABI
+// (include/ghostm_hip.h Part 1 + the device-level extensions of Part 2).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/ghostm_hip.h"
+#include "common.h"
+#include "device.h"
+#include "formats.h"
+#include "kernels.h"
+
+namespace ghostm {
+
+#define HIP_CHECK(expr)                                                                  \
+  do {                                                                                   \
+    hipError_t err_ = (expr);                                                            \
+    if (err_ != hipSuccess)                                                              \
+      throw Error(std::string("HIP error '") + hipGetErrorString(err_) + "' at " #expr); \
+  } while (0)
+
+namespace {
+
+struct DevBuf {
+  void *p = nullptr;
+  size_t bytes = 0;
+  void Reserve(size_t b) {
+    if (b <= bytes) return;
+    if (p) HIP_CHECK(hipFree(p));
+    p = nullptr;
+    bytes = 0;
+    size_t want = std::max<size_t>(b, 256);
+    HIP_CHECK(hipMalloc(&p, want));
+    bytes = want;
+  }
+  void Release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <class T> T *as() const { return static_cast<T *>(p); }
+};
+
+// Rows per lane (S) and lanes per candidate (G) for a query width L: the layout
+// with the fewest lane-steps per useful cell among S in {8, 16, 32}.
+struct Layout {
+  int S;
+  uint32_t G, Lpad, gpw;
+};
+
+Layout ChooseLayout(uint32_t L, uint32_t width) {
+  Layout best{32, 1, 32, 64};
+  double best_cost = 1e300;
+  for (int S : {32, 16, 8}) {
+    const uint32_t G = (L + S - 1) / S;
+    if (G == 0 || G > 16) continue;
+    const uint32_t gpw = 64 / G;
+    const double cost = (double)(G * S) * (double)(width + G - 1) / (double)(gpw * G);
+    if (cost < best_cost * 0.999) {
+      best_cost = cost;
+      best = Layout{S, G, G * (uint32_t)S, gpw};
+    }
+  }
+  return best;
+}
+
+thread_local std::string g_last_error;
+
+}  // namespace
+
+struct DevQuery {
+  DevBuf seq;
+  uint32_t nseq = 0, L = 0;
+};
+
+struct DevDb {
+  DevBuf seq, kc, pos;
+  uint32_t len = 0, kcl = 0, npos = 0;
+};
+
+struct DeviceModule::Impl {
+  int h_matrix[32 * 32] = {0};
+  DevBuf mat_k2, mat_tb;
+  // K1 work
+  DevBuf counts, nelem, slots, offsets, qlist, gbuf, gbuf_off;
+  DevBuf cand_start, cand_qid;
+  uint64_t ncand = 0;
+  // K2 work
+  DevBuf tasks, score_out, end_out;
+  // K3 work
+  DevBuf tb_qid, tb_end, tb_start, tb_ml;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool matrix_set = false;
+};
+
+static constexpr uint32_t kSlotCap = 256;
+
+DeviceModule &DeviceModule::Get() {
+  static DeviceModule *m = new DeviceModule();
+  return *m;
+}
+
+void DeviceModule::Bind(int device) {
+  if (device_ == device && impl_) return;
+  int n = 0;
+  HIP_CHECK(hipGetDeviceCount(&n));
+  if (n <= 0) throw Error("no HIP device visible");
+  if (device < 0 || device >= n) throw Error("device id " + std::to_string(device) + " out of range");
+  HIP_CHECK(hipSetDevice(device));
+  if (!impl_) impl_ = new Impl();
+  hipStream_t s;
+  HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  stream_ = s;
+  HIP_CHECK(hipEventCreate(&impl_->ev0));
+  HIP_CHECK(hipEventCreate(&impl_->ev1));
+  HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_seed<false>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                2 * kern::kSeedLdsCap * 4));
+  device_ = device;
+}
+
+static hipStream_t S(void *s) { return static_cast<hipStream_t>(s); }
+
+std::string DeviceModule::DeviceName() const {
+  hipDeviceProp_t p;
+  HIP_CHECK(hipGetDeviceProperties(&p, device_ < 0 ? 0 : device_));
+  return std::string(p.name) + " (" + p.gcnArchName + ")";
+}
+
+size_t DeviceModule::TotalMemory() const {
+  hipDeviceProp_t p;
+  HIP_CHECK(hipGetDeviceProperties(&p, device_ < 0 ? 0 : device_));
+  return p.totalGlobalMem;
+}
+
+void DeviceModule::SetMatrix(const int *m) {
+  if (!impl_) throw Error("device not bound");
+  std::memcpy(impl_->h_matrix, m, sizeof(impl_->h_matrix));
+  int k2[32 * 32], tb[32 * 32];
+  for (int c = 0; c < 32; ++c) {
+    for (int q = 0; q < 32; ++q) {
+      const int v = m[c * 32 + q];
+      k2[c * 32 + q] = q == (int)kern::kPadCode ? kern::kNeg : v;
+      const int inc = 0x100 | (c == q ? 1 : 0);
+      tb[c * 32 + q] = q == (int)kern::kPadCode ? (int)((unsigned)kern::kNeg << 16)
+                                                : (int)(((unsigned)v << 16) | (unsigned)inc);
+    }
+  }
+  impl_->mat_k2.Reserve(sizeof(k2));
+  impl_->mat_tb.Reserve(sizeof(tb));
+  HIP_CHECK(hipMemcpy(impl_->mat_k2.p, k2, sizeof(k2), hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(impl_->mat_tb.p, tb, sizeof(tb), hipMemcpyHostToDevice));
+  impl_->matrix_set = true;
+}
+
+DevQuery *DeviceModule::UploadQuery(const uint8_t *seq, uint32_t nseq, uint32_t L) {
+  if (!impl_) throw Error("device not bound");
+  if (L == 0 || L > kMaxQueryLength)
+    throw Error("query record width " + std::to_string(L) + " outside 1..127");
+  DevQuery *q = new DevQuery();
+  q->nseq = nseq;
+  q->L = L;
+  const size_t b = (size_t)nseq * L;
+  q->seq.Reserve(b + 16);
+  if (b) HIP_CHECK(hipMemcpy(q->seq.p, seq, b, hipMemcpyHostToDevice));
+  return q;
+}
+
+DevDb *DeviceModule::UploadDb(const uint8_t *seq, uint32_t len, const uint32_t *kc, uint32_t kcl,
+                              const uint32_t *pos, uint32_t npos) {
+  if (!impl_) throw Error("device not bound");
+  DevDb *d = new DevDb();
+  d->len = len;
+  d->kcl = kcl;
+  d->npos = npos;
+  d->seq.Reserve((size_t)len + 16);
+  d->kc.Reserve((size_t)kcl * 4);
+  d->pos.Reserve((size_t)npos * 4 + 4);
+  if (len) HIP_CHECK(hipMemcpy(d->seq.p, seq, len, hipMemcpyHostToDevice));
+  if (kcl) HIP_CHECK(hipMemcpy(d->kc.p, kc, (size_t)kcl * 4, hipMemcpyHostToDevice));
+  if (npos) HIP_CHECK(hipMemcpy(d->pos.p, pos, (size_t)npos * 4, hipMemcpyHostToDevice));
+  return d;
+}
+
+void DeviceModule::Free(DevQuery *q) {
+  if (!q) return;
+  q->seq.Release();
+  delete q;
+}
+
+void DeviceModule::Free(DevDb *d) {
+  if (!d) return;
+  d->seq.Release();
+  d->kc.Release();
+  d->pos.Release();
+  delete d;
+}
+
+void DeviceModule::Synchronize() {
+  if (stream_) HIP_CHECK(hipStreamSynchronize(S(stream_)));
+}
+
+static float ElapsedMs(hipEvent_t a, hipEvent_t b) {
+  float ms = 0;
+  HIP_CHECK(hipEventSynchronize(b));
+  HIP_CHECK(hipEventElapsedTime(&ms, a, b));
+  return ms;
+}
+
+uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
+                            std::vector<uint32_t> *counts, std::vector<uint64_t> *offsets) {
+  Impl &I = *impl_;
+  const uint32_t nq = q->nseq;
+  counts->assign(nq, 0);
+  offsets->assign(nq, 0);
+  I.ncand = 0;
+  if (nq == 0) return 0;
+  const uint32_t seed_len = [](uint32_t s) { uint32_t n = 0; for (; s; s >>= 1) ++n; return n; }(cfg.seed_mask);
+  if (seed_len == 0 || seed_len > q->L) return 0;
+  if (cfg.shift == 0) throw Error("shift size must be positive");
+  const uint32_t nlists = (q->L - seed_len) / cfg.shift + 1;
+  if (nlists > kern::kMaxLists) throw Error("too many seed lists");
+  if (d->kcl == 0) throw Error("database index missing");
+
+  I.counts.Reserve((size_t)nq * 4);
+  I.nelem.Reserve((size_t)nq * 4);
+  I.slots.Reserve((size_t)nq * kSlotCap * 4);
+  I.offsets.Reserve((size_t)nq * 8);
+  HIP_CHECK(hipMemsetAsync(I.nelem.p, 0, (size_t)nq * 4, S(stream_)));
+
+  kern::SeedArgs a{};
+  a.qseq = q->seq.as<uint8_t>();
+  a.L = q->L;
+  a.keys_count = d->kc.as<uint32_t>();
+  a.positions = d->pos.as<uint32_t>();
+  a.seed_mask = cfg.seed_mask;
+  a.nlists = nlists;
+  a.shift = cfg.shift;
+  a.log_region = cfg.log_region;
+  a.threshold = cfg.threshold;
+  a.counts = I.counts.as<uint32_t>();
+  a.nelem = I.nelem.as<uint32_t>();
+  a.slots = I.slots.as<uint32_t>();
+  a.slot_cap = kSlotCap;
+  const size_t lds = 2 * kern::kSeedLdsCap * 4;
+
+  HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
+  // pass 1: every query, LDS merge, candidates into per-query slots
+  hipLaunchKernelGGL(kern::k_seed<false>, dim3(nq), dim3(kern::kSeedBlock), lds, S(stream_), a);
+  HIP_CHECK(hipGetLastError());
+  std::vector<uint32_t> nel(nq);
+  HIP_CHECK(hipMemcpyAsync(counts->data(), I.counts.p, (size_t)nq * 4, hipMemcpyDeviceToHost, S(stream_)));
+  HIP_CHECK(hipMemcpyAsync(nel.data(), I.nelem.p, (size_t)nq * 4, hipMemcpyDeviceToHost, S(stream_)));
+  HIP_CHECK(hipStreamSynchronize(S(stream_)));
+
+  // pass 2: queries whose bins exceed LDS -> global merge buffers (count only)
+  std::vector<uint32_t> big, wide;
+  std::vector<unsigned long long> goff;
+  unsigned long long gtotal = 0;
+  uint64_t bins_total = 0;
+  for (uint32_t i = 0; i < nq; ++i) {
+    if ((*counts)[i] == kern::kOverflow) {
+      big.push_back(i);
+      goff.push_back(gtotal);
+      gtotal += 2ull * nel[i];
+    }
+  }
+  auto run_global = [&](bool write) {
+    if (big.empty()) return;
+    I.qlist.Reserve(big.size() * 4);
+    I.gbuf_off.Reserve(goff.size() * 8);
+    I.gbuf.Reserve(gtotal * 4);
+    HIP_CHECK(hipMemcpyAsync(I.qlist.p, big.data(), big.size() * 4, hipMemcpyHostToDevice, S(stream_)));
+    HIP_CHECK(hipMemcpyAsync(I.gbuf_off.p, goff.data(), goff.size() * 8, hipMemcpyHostToDevice, S(stream_)));
+    kern::SeedArgs b = a;
+    b.query_list = I.qlist.as<uint32_t>();
+    b.gbuf = I.gbuf.as<uint32_t>();
+    b.gbuf_off = I.gbuf_off.as<unsigned long long>();
+    b.slots = nullptr;
+    if (write) {
+      b.offsets = I.offsets.as<unsigned long long>();
+      b.out_start = I.cand_start.as<uint32_t>();
+      b.out_qid = I.cand_qid.as<uint32_t>();
+    }
+    hipLaunchKernelGGL(kern::k_seed<true>, dim3((uint32_t)big.size()), dim3(kern::kSeedBlock), 0,
+                       S(stream_), b);
+    HIP_CHECK(hipGetLastError());
+  };
+  if (!big.empty()) {
+    run_global(false);
+    std::vector<uint32_t> c2(nq);
+    HIP_CHECK(hipMemcpyAsync(c2.data(), I.counts.p, (size_t)nq * 4, hipMemcpyDeviceToHost, S(stream_)));
+    HIP_CHECK(hipStreamSynchronize(S(stream_)));
+    for (uint32_t i : big) (*counts)[i] = c2[i];
+  }
+  uint64_t total = 0;
+  for (uint32_t i = 0; i < nq; ++i) {
+    (*offsets)[i] = total;
+    total += (*counts)[i];
+    if ((*counts)[i] > kSlotCap && nel[i] == 0) wide.push_back(i);
+    bins_total += nel[i];
+  }
+  I.ncand = total;
+  I.cand_start.Reserve(total * 4 + 4);
+  I.cand_qid.Reserve(total * 4 + 4);
+  HIP_CHECK(hipMemcpyAsync(I.offsets.p, offsets->data(), (size_t)nq * 8, hipMemcpyHostToDevice, S(stream_)));
+  // pass 3: slot -> compact
+  hipLaunchKernelGGL(kern::k_compact, dim3((nq + 3) / 4), dim3(256), 0, S(stream_),
+                     I.slots.as<uint32_t>(), kSlotCap, I.counts.as<uint32_t>(),
+                     I.nelem.as<uint32_t>(), I.offsets.as<unsigned long long>(), nq,
+                     I.cand_start.as<uint32_t>(), I.cand_qid.as<uint32_t>());
+  HIP_CHECK(hipGetLastError());
+  // pass 4: queries with more candidates than a slot -> rerun straight into place
+  if (!wide.empty()) {
+    I.qlist.Reserve(wide.size() * 4);
+    HIP_CHECK(hipMemcpyAsync(I.qlist.p, wide.data(), wide.size() * 4, hipMemcpyHostToDevice, S(stream_)));
+    kern::SeedArgs b = a;
+    b.query_list = I.qlist.as<uint32_t>();
+    b.slots = nullptr;
+    b.offsets = I.offsets.as<unsigned long long>();
+    b.out_start = I.cand_start.as<uint32_t>();
+    b.out_qid = I.cand_qid.as<uint32_t>();
+    hipLaunchKernelGGL(kern::k_seed<false>, dim3((uint32_t)wide.size()), dim3(kern::kSeedBlock), lds,
+                       S(stream_), b);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipStreamSynchronize(S(stream_)));
+  }
+  // pass 5: LDS-overflow queries, written from global merge buffers
+  run_global(true);
+  HIP_CHECK(hipEventRecord(I.ev1, S(stream_)));
+  times_.seed += ElapsedMs(I.ev0, I.ev1) * 1e-3;
+  // algorithmic bytes: query record + 2 CSR words per list + positions + outputs
+  (void)bins_total;
+  times_.seed_bytes += (uint64_t)nq * (q->L + 8ull * nlists + 4) + total * 8ull;
+  return total;
+}
+
+void DeviceModule::CopyStarts(uint64_t begin, uint64_t n, uint32_t *out) {
+  if (n == 0) return;
+  HIP_CHECK(hipMemcpy(out, impl_->cand_start.as<uint32_t>() + begin, n * 4, hipMemcpyDeviceToHost));
+}
+
+void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n, uint32_t q_first,
+                         uint32_t q_end, const std::vector<uint32_t> &counts,
+                         const std::vector<uint64_t> &offsets, uint32_t base,
+                         const GapConfig &gap, uint32_t *score, uint32_t *end) {
+  Impl &I = *impl_;
+  if (n == 0) return;
+  if (gap.ext > 0) throw Error("positive gap extension score is not supported");
+  const Layout lay = ChooseLayout(q->L, base);
+  const uint32_t per_block = (kern::kScoreBlock / 64) * lay.gpw;
+  // tasks: runs of <= per_block consecutive candidates spanning <= Qmax queries
+  std::vector<kern::ScoreTask> tasks;
+  tasks.reserve(n / per_block + (q_end - q_first) / kern::kScoreQmax + 2);
+  kern::ScoreTask cur{};
+  bool open_task = false;
+  auto flush = [&]() {
+    if (open_task && cur.count) tasks.push_back(cur);
+    open_task = false;
+  };
+  const uint64_t cand_end = cand_begin + n;
+  for (uint32_t qi = q_first; qi < q_end; ++qi) {
+    uint64_t lo = std::max<uint64_t>(offsets[qi], cand_begin);
+    const uint64_t hi = std::min<uint64_t>(offsets[qi] + counts[qi], cand_end);
+    while (lo < hi) {
+      if (open_task && (cur.count == per_block || qi - cur.q_first >= (uint32_t)kern::kScoreQmax)) flush();
+      if (!open_task) {
+        cur = kern::ScoreTask{};
+        cur.begin = lo;
+        cur.q_first = qi;
+        open_task = true;
+      }
+      const uint64_t take = std::min<uint64_t>(hi - lo, per_block - cur.count);
+      cur.count += (uint32_t)take;
+      cur.q_count = qi - cur.q_first + 1;
+      lo += take;
+    }
+  }
+  flush();
+  I.tasks.Reserve(tasks.size() * sizeof(kern::ScoreTask));
+  I.score_out.Reserve(n * 4);
+  I.end_out.Reserve(n * 4);
+  HIP_CHECK(hipMemcpyAsync(I.tasks.p, tasks.data(), tasks.size() * sizeof(kern::ScoreTask),
+                           hipMemcpyHostToDevice, S(stream_)));
+  kern::ScoreArgs a{};
+  a.qseq = q->seq.as<uint8_t>();
+  a.L = q->L;
+  a.Lpad = lay.Lpad;
+  a.pad = lay.Lpad - q->L;
+  a.G = lay.G;
+  a.gpw = lay.gpw;
+  a.db = d->seq.as<uint8_t>();
+  a.dblen = d->len;
+  a.mat = I.mat_k2.as<int>();
+  a.cand_qid = I.cand_qid.as<uint32_t>();
+  a.cand_start = I.cand_start.as<uint32_t>();
+  a.tasks = I.tasks.as<kern::ScoreTask>();
+  a.base = base;
+  a.extend = gap.extend;
+  a.open = gap.open;
+  a.ext = gap.ext;
+  a.score_out = I.score_out.as<uint32_t>();
+  a.end_out = I.end_out.as<uint32_t>();
+  a.out_base = cand_begin;
+  const size_t lds = (size_t)kern::kScoreQmax * kern::kProfRows * (lay.Lpad + 4) * 4;
+  HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
+  const dim3 grid((uint32_t)tasks.size()), block(kern::kScoreBlock);
+  switch (lay.S) {
+    case 32: hipLaunchKernelGGL(kern::k_score<32>, grid, block, lds, S(stream_), a); break;
+    case 16: hipLaunchKernelGGL(kern::k_score<16>, grid, block, lds, S(stream_), a); break;
+    default: hipLaunchKernelGGL(kern::k_score<8>, grid, block, lds, S(stream_), a); break;
+  }
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipEventRecord(I.ev1, S(stream_)));
+  HIP_CHECK(hipMemcpyAsync(score, I.score_out.p, n * 4, hipMemcpyDeviceToHost, S(stream_)));
+  HIP_CHECK(hipMemcpyAsync(end, I.end_out.p, n * 4, hipMemcpyDeviceToHost, S(stream_)));
+  HIP_CHECK(hipStreamSynchronize(S(stream_)));
+  times_.score += ElapsedMs(I.ev0, I.ev1) * 1e-3;
+  times_.score_launches += 1;
+}
+
+void DeviceModule::TraceBack(DevQuery *q, DevDb *d, uint32_t n, const uint32_t *qid,
+                             const uint32_t *db_end, uint32_t base, int open, int ext,
+                             uint32_t *db_start, uint32_t *aln_len, uint32_t *aln_match,
+                             float *seq_id) {
+  Impl &I = *impl_;
+  if (n == 0) return;
+  const Layout lay = ChooseLayout(q->L, base);
+  I.tb_qid.Reserve((size_t)n * 4);
+  I.tb_end.Reserve((size_t)n * 4);
+  I.tb_start.Reserve((size_t)n * 4);
+  I.tb_ml.Reserve((size_t)n * 4);
+  HIP_CHECK(hipMemcpyAsync(I.tb_qid.p, qid, (size_t)n * 4, hipMemcpyHostToDevice, S(stream_)));
+  HIP_CHECK(hipMemcpyAsync(I.tb_end.p, db_end, (size_t)n * 4, hipMemcpyHostToDevice, S(stream_)));
+  kern::TbArgs a{};
+  a.qseq = q->seq.as<uint8_t>();
+  a.L = q->L;
+  a.Lpad = lay.Lpad;
+  a.G = lay.G;
+  a.gpw = lay.gpw;
+  a.db = d->seq.as<uint8_t>();
+  a.mat_tb = I.mat_tb.as<int>();
+  a.qid = I.tb_qid.as<uint32_t>();
+  a.end = I.tb_end.as<uint32_t>();
+  a.n = n;
+  a.base = base;
+  a.open = open;
+  a.ext = ext;
+  a.out_start = I.tb_start.as<uint32_t>();
+  a.out_ml = I.tb_ml.as<uint32_t>();
+  const uint32_t per_block = (kern::kTbBlock / 64) * lay.gpw;
+  const dim3 grid((n + per_block - 1) / per_block), block(kern::kTbBlock);
+  HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
+  switch (lay.S) {
+    case 32: hipLaunchKernelGGL(kern::k_traceback<32>, grid, block, 0, S(stream_), a); break;
+    case 16: hipLaunchKernelGGL(kern::k_traceback<16>, grid, block, 0, S(stream_), a); break;
+    default: hipLaunchKernelGGL(kern::k_traceback<8>, grid, block, 0, S(stream_), a); break;
+  }
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipEventRecord(I.ev1, S(stream_)));
+  std::vector<uint32_t> ml(n);
+  HIP_CHECK(hipMemcpyAsync(db_start, I.tb_start.p, (size_t)n * 4, hipMemcpyDeviceToHost, S(stream_)));
+  HIP_CHECK(hipMemcpyAsync(ml.data(), I.tb_ml.p, (size_t)n * 4, hipMemcpyDeviceToHost, S(stream_)));
+  HIP_CHECK(hipStreamSynchronize(S(stream_)));
+  times_.traceback += ElapsedMs(I.ev0, I.ev1) * 1e-3;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t len = ml[i] >> 8, match = ml[i] & 0xFFu;
+    if (aln_len) aln_len[i] = len;
+    if (aln_match) aln_match[i] = match;
+    // seq_id as the reference computes it on the host (aligner.cpp:945)
+    if (seq_id) seq_id[i] = (float)match / (float)len;
+  }
+}
+
+const char *DeviceBuildInfo() {
+  return "ghostm_hip gfx950: K1 k_seed<LDS|global merge-path>, K2 k_score<S=8|16|32> "
+         "lane-group int32, K3 k_traceback<S=8|16|32>";
+}
+
+// ============================================================ reference C ABI
+namespace {
+
+struct RefState {
+  std::mutex mu;
+  uint32_t max_list_length = 0;
+  DevQuery *query = nullptr;
+  DevDb *db = nullptr;
+  bool seeded = false;
+  std::vector<uint32_t> counts;
+  std::vector<uint64_t> offsets;
+  // last batch (SearchNextGpu)
+  uint32_t batch_first = 0, batch_count = 0;
+  uint64_t batch_begin = 0, batch_n = 0;
+};
+
+RefState &Ref() {
+  static RefState *s = new RefState();
+  return *s;
+}
+
+void SetError(const std::string &m) { g_last_error = m; }
+
+}  // namespace
+
+void SetLastErrorMessage(const std::string &m) { g_last_error = m; }
+
+}  // namespace ghostm
+
+using namespace ghostm;
+
+extern "C" {
+
+const char *GhostmGetLastError(void) { return g_last_error.c_str(); }
+
+const char *GhostmBuildInfo(void) { return DeviceBuildInfo(); }
+
+int InitGpu(void) {
+  RefState &r = Ref();
+  std::lock_guard<std::mutex> lk(r.mu);
+  DeviceModule &m = DeviceModule::Get();
+  if (r.query) m.Free(r.query);
+  if (r.db) m.Free(r.db);
+  r.query = nullptr;
+  r.db = nullptr;
+  r.seeded = false;
+  r.counts.clear();
+  r.offsets.clear();
+  g_last_error.clear();
+  return 0;
+}
+
+size_t GetNeededGPUMemorySize(uint32_t seed, uint32_t shift_size, uint32_t max_list_length,
+                              uint32_t max_query_length, uint32_t max_number_queries,
+                              uint32_t max_db_length) {
+  const uint32_t w = SeedWeight(seed);
+  uint64_t kcl = 1;
+  for (uint32_t i = 0; i < w; ++i) kcl *= 32;
+  kcl += 1;
+  const uint32_t seed_len = SeedLength(seed);
+  const uint64_t nq = max_number_queries;
+  const uint64_t lists = max_query_length >= seed_len && shift_size
+                             ? (max_query_length - seed_len) / shift_size + 1
+                             : 0;
+  (void)lists;
+  size_t b = 0;
+  b += (size_t)nq * max_query_length;             // query records
+  b += (size_t)nq * (4 + 4 + 8 + 256 * 4);          // counts, nelem, offsets, slots
+  b += (size_t)max_list_length * 16;                // start, qid, score, end
+  b += (size_t)max_db_length * (1 + 4);             // sequence + positions
+  b += (size_t)kcl * 4;                             // CSR offsets
+  b += 2 * 32 * 32 * 4;                             // score tables
+  return b;
+}
+
+int CheckGpuMemory(uint32_t seed, uint32_t shift_size, uint32_t max_list_length,
+                   uint32_t max_query_length, uint32_t max_number_queries, uint32_t max_db_length) {
+  try {
+    size_t free_b = 0, total_b = 0;
+    int dev = DeviceModule::Get().device();
+    if (dev < 0) HIP_CHECK(hipSetDevice(0));
+    HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+    return GetNeededGPUMemorySize(seed, shift_size, max_list_length, max_query_length,
+                                  max_number_queries, max_db_length) > total_b ? 1 : 0;
+  } catch (std::exception &e) {
+    SetError(e.what());
+    return 1;
+  }
+}
+
+int SetOptionGpu(uint32_t max_list_length, int score_matrix[], int device) {
+  try {
+    RefState &r = Ref();
+    std::lock_guard<std::mutex> lk(r.mu);
+    DeviceModule &m = DeviceModule::Get();
+    m.Bind(device);
+    m.SetMatrix(score_matrix);
+    r.max_list_length = max_list_length;
+    return 0;
+  } catch (std::exception &e) {
+    SetError(e.what());
+    return 1;
+  }
+}
+
+void printGpuInfo(int device) {
+  try {
+    hipDeviceProp_t p;
+    HIP_CHECK(hipGetDeviceProperties(&p, device));
+    fprintf(stdout, "  [GPU] device: \"%s\"\n", p.name);
+    fprintf(stdout, "  [GPU] global memory size: %lu bytes (%gMB)\n", (unsigned long)p.totalGlobalMem,
+            p.totalGlobalMem / 1048576.0);
+  } catch (std::exception &e) {
+    SetError(e.what());
+  }
+}
+
+int SetQueryGpu(uint8_t sequences[], uint32_t number_sequences, uint32_t sequence_length) {
+  try {
+    RefState &r = Ref();
+    std::lock_guard<std::mutex> lk(r.mu);
+    DeviceModule &m = DeviceModule::Get();
+    if (r.query) m.Free(r.query);
+    r.query = m.UploadQuery(sequences, number_sequences, sequence_length);
+    r.seeded = false;
+    return 0;
+  } catch (std::exception &e) {
+    SetError(e.what());
+    return 1;
+  }
+}
+
+int SetDbGpu(uint8_t sequences[], uint32_t sequences_legnth, uint32_t keys_count[],
+             uint32_t keys_count_length, uint32_t positions[], uint32_t positions_length) {
+  try {
+    RefState &r = Ref();
+    std::lock_guard<std::mutex> lk(r.mu);
+    DeviceModule &m = DeviceModule::Get();
+    if (r.db) m.Free(r.db);
+    r.db = m.UploadDb(sequences, sequences_legnth, keys_count, keys_count_length, positions,
+                      positions_length);
+    r.seeded = false;
+    return 0;
+  } catch (std::exception &e) {
+    SetError(e.what());
+    return 1;
+  }
+}
+
+uint32_t SearchNextGpu(uint32_t query_sequence_length, uint32_t number_query_sequences,
+                       uint32_t seed, uint32_t threshold, uint32_t shift_size,
+                       uint32_t log_region_size, uint32_t max_number_alignments,
+                       uint32_t start_query_id, uint32_t *alignment_count_list, uint32_t *starts) {
+  try {
+    RefState &r = Ref();
+    std::lock_guard<std::mutex> lk(r.mu);
+    if (!r.query || !r.db) throw Error("SetQueryGpu/SetDbGpu not called");
+    if (start_query_id >= number_query_sequences) return 0;
+    if (query_sequence_length != r.query->L || number_query_sequences != r.query->nseq)
+      throw Error("query shape differs from SetQueryGpu");
+    DeviceModule &m = DeviceModule::Get();
+    if (!r.seeded || start_query_id == 0) {
+      SeedConfig cfg;
+      cfg.seed_mask = seed;
+      cfg.threshold = threshold;
+      cfg.shift = shift_size;
+      cfg.log_region = log_region_size;
+      m.Seed(r.query, r.db, cfg, &r.counts, &r.offsets);
+      r.seeded = true;
+    }
+    // reference GPU batching rule (aligner_gpu.cu:911-920)
+    uint64_t total = 0;
+    uint32_t j = 1;
+    alignment_count_list[0] = 0;
+    for (uint32_t i = start_query_id; i < number_query_sequences; ++i, ++j) {
+      if (total + r.counts[i] >= max_number_alignments) break;
+      total += r.counts[i];
+      alignment_count_list[j] = (uint32_t)total;
+    }
+    const uint32_t qcount = j - 1;
+    r.batch_first = start_query_id;
+    r.batch_count = qcount;
+    r.batch_begin = r.offsets[start_query_id];
+    r.batch_n = total;
+    m.CopyStarts(r.batch_begin, total, starts);
+    return qcount;
+  } catch (std::exception &e) {
+    SetError(e.what());
+    fprintf(stderr, "[ghostm_hip] SearchNextGpu: %s\n", e.what());
+    return 0;
+  }
+}
+
+void CalculateScoreGpu(uint32_t db_length, uint32_t query_sequence_length,
+                       uint32_t number_alignment_list, uint32_t scores[], uint32_t ends[],
+                       uint32_t base_search_length, uint32_t offset, int open_gap, int extend_gap) {
+  try {
+    RefState &r = Ref();
+    std::lock_guard<std::mutex> lk(r.mu);
+    if (!r.seeded) throw Error("SearchNextGpu not called");
+    (void)db_length;
+    (void)query_sequence_length;
+    GapConfig gap;
+    gap.extend = offset;
+    gap.open = open_gap;
+    gap.ext = extend_gap;
+    const uint64_t n = std::min<uint64_t>(number_alignment_list, r.batch_n);
+    DeviceModule::Get().Score(r.query, r.db, r.batch_begin, n, r.batch_first,
+                              r.batch_first + r.batch_count, r.counts, r.offsets,
+                              base_search_length, gap, scores, ends);
+  } catch (std::exception &e) {
+    SetError(e.what());
+    fprintf(stderr, "[ghostm_hip] CalculateScoreGpu: %s\n", e.what());
+  }
+}
+
+int FreeGpu(void) {
+  try {
+    RefState &r = Ref();
+    std::lock_guard<std::mutex> lk(r.mu);
+    DeviceModule &m = DeviceModule::Get();
+    if (r.query) m.Free(r.query);
+    if (r.db) m.Free(r.db);
+    r.query = nullptr;
+    r.db = nullptr;
+    r.seeded = false;
+    return 0;
+  } catch (std::exception &e) {
+    SetError(e.what());
+    return 1;
+  }
+}
+
+int CountCandidatesGpu(uint32_t query_sequence_length, uint32_t number_query_sequences,
+                       uint32_t seed, uint32_t threshold, uint32_t shift_size,
+                       uint32_t log_region_size, uint32_t counts[]) {
+  try {
+    RefState &r = Ref();
+    std::lock_guard<std::mutex> lk(r.mu);
+    if (!r.query || !r.db) throw Error("SetQueryGpu/SetDbGpu not called");
+    if (query_sequence_length != r.query->L || number_query_sequences != r.query->nseq)
+      throw Error("query shape differs from SetQueryGpu");
+    SeedConfig cfg;
+    cfg.seed_mask = seed;
+    cfg.threshold = threshold;
+    cfg.shift = shift_size;
+    cfg.log_region = log_region_size;
+    DeviceModule::Get().Seed(r.query, r.db, cfg, &r.counts, &r.offsets);
+    r.seeded = true;
+    std::copy(r.counts.begin(), r.counts.end(), counts);
+    return 0;
+  } catch (std::exception &e) {
+    SetError(e.what());
+    return 1;
+  }
+}
+
+int TraceBackGpu(uint32_t nhits, const uint32_t query_ids[], const uint32_t db_ends[],
+                 uint32_t query_sequence_length, uint32_t base_search_length, int open_gap,
+                 int extend_gap, uint32_t db_starts[], uint32_t aln_lens[],
+                 uint32_t aln_matches[], float seq_ids[]) {
+  try {
+    RefState &r = Ref();
+    std::lock_guard<std::mutex> lk(r.mu);
+    if (!r.query || !r.db) throw Error("SetQueryGpu/SetDbGpu not called");
+    if (query_sequence_length != r.query->L) throw Error("query shape differs from SetQueryGpu");
+    DeviceModule::Get().TraceBack(r.query, r.db, nhits, query_ids, db_ends, base_search_length,
+                                  open_gap, extend_gap, db_starts, aln_lens, aln_matches, seq_ids);
+    return 0;
+  } catch (std::exception &e) {
+    SetError(e.what());
+    return 1;
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,152 @@
+// formats.cpp — see formats.h for the layouts and the reference citations.
+#include "formats.h"
+
+#include <climits>
+#include <fstream>
+#include <iostream>
+
+#include "common.h"
+
+namespace ghostm {
+
+uint8_t ProteinCode(unsigned char ch) {
+  struct Table {
+    uint8_t t[256];
+    Table() {
+      const char *order = "ARNDCQEGHILKMFPSTWYVBJZX*";
+      for (int i = 0; i < 256; ++i) t[i] = kBaseX;
+      for (int i = 0; order[i]; ++i) {
+        unsigned char u = (unsigned char)order[i];
+        t[u] = (uint8_t)i;
+        if (u >= 'A' && u <= 'Z') t[u + 32] = (uint8_t)i;
+      }
+    }
+  };
+  static const Table table;
+  return table.t[ch];
+}
+
+uint8_t DnaCode(unsigned char ch) {
+  switch (ch) {
+    case 'A': case 'a': return 0;
+    case 'C': case 'c': return 1;
+    case 'G': case 'g': return 2;
+    case 'T': case 't': return 3;
+    case '-': return 5;
+    default: return 4;
+  }
+}
+
+uint32_t SeedLength(uint32_t seed) {
+  uint32_t n = 0;
+  for (; seed; seed >>= 1) ++n;
+  return n;
+}
+
+uint32_t SeedWeight(uint32_t seed) {
+  uint32_t n = 0;
+  for (; seed; seed >>= 1) n += seed & 1;
+  return n;
+}
+
+template <class T>
+static void ReadRaw(std::ifstream &f, T *p, size_t count) {
+  f.read(reinterpret_cast<char *>(p), sizeof(T) * count);
+}
+
+std::vector<std::string> ReadNameLines(const std::string &path, uint32_t n, bool *complete) {
+  std::vector<std::string> names(n);
+  std::ifstream f(path.c_str());
+  if (complete) *complete = true;
+  if (!f) return names;
+  uint32_t i = 0;
+  std::string line;
+  for (; i < n && !f.eof(); ++i) {
+    std::getline(f, line);
+    names[i].swap(line);
+  }
+  if (i < n) {
+    std::cerr << "warning : couldn't read all sequence names" << std::endl;
+    if (complete) *complete = false;
+  }
+  return names;
+}
+
+QueryFile::QueryFile(const std::string &p) : prefix(p) {
+  std::ifstream f((p + ".inf").c_str(), std::ios::binary);
+  if (!f) return;
+  ReadRaw(f, &division, 1);
+  ReadRaw(f, &max_length, 1);
+  ReadRaw(f, &max_nseq, 1);
+}
+
+bool QueryFile::ReadChunk(uint32_t id, QueryChunk *q) const {
+  if (id >= division) return false;
+  const std::string base = prefix + "_" + std::to_string(id);
+  std::ifstream f((base + ".inf").c_str(), std::ios::binary);
+  if (!f) return false;
+  q->id = id;
+  ReadRaw(f, &q->nseq, 1);
+  ReadRaw(f, &q->L, 1);
+  q->names = ReadNameLines(base + ".nam", q->nseq, nullptr);
+  q->seq.assign((size_t)q->nseq * q->L, 0);
+  std::ifstream s((base + ".seq").c_str(), std::ios::binary);
+  if (s) ReadRaw(s, q->seq.data(), q->seq.size());
+  return true;
+}
+
+DbFile::DbFile(const std::string &p) : prefix(p) {
+  std::ifstream f((p + ".inf").c_str(), std::ios::binary);
+  if (!f) return;
+  ReadRaw(f, &division, 1);
+  ReadRaw(f, &seed, 1);
+  ReadRaw(f, &max_length, 1);
+  ReadRaw(f, &sum_length, 1);
+}
+
+bool DbFile::ReadChunk(uint32_t id, DbChunk *d) const {
+  if ((int64_t)id >= (int64_t)division) return false;
+  const std::string base = prefix + "_" + std::to_string(id);
+  std::ifstream f((base + ".inf").c_str(), std::ios::binary);
+  if (!f) return false;
+  d->id = id;
+  ReadRaw(f, &d->nseq, 1);
+  ReadRaw(f, &d->len, 1);
+  d->names = ReadNameLines(base + ".nam", d->nseq, nullptr);
+  d->starts.assign(d->nseq, 0);
+  {
+    std::ifstream s((base + ".pos").c_str(), std::ios::binary);
+    if (s) ReadRaw(s, d->starts.data(), d->nseq);
+  }
+  d->seq.assign(d->len, 0);
+  {
+    std::ifstream s((base + ".seq").c_str(), std::ios::binary);
+    if (s) ReadRaw(s, d->seq.data(), d->len);
+  }
+  std::ifstream s((base + ".ind").c_str(), std::ios::binary);
+  if (s) {
+    ReadRaw(s, &d->seed, 1);
+    ReadRaw(s, &d->kcl, 1);
+    ReadRaw(s, &d->npos, 1);
+    d->keys_count.assign(d->kcl, 0);
+    d->positions.assign(d->npos, 0);
+    ReadRaw(s, d->keys_count.data(), d->kcl);
+    ReadRaw(s, d->positions.data(), d->npos);
+  }
+  return true;
+}
+
+uint32_t DbChunk::SubjectOf(uint32_t p) const {
+  // Same search as DB::GetID: the last subject first, then a u32 binary search.
+  if (starts[nseq - 1] <= p && p < len) return nseq - 1;
+  uint32_t lo = 0, hi = nseq - 2;
+  while (lo <= hi) {
+    const uint32_t mid = (lo + hi) / 2;
+    if (starts[mid] <= p && p < starts[mid + 1]) return mid;
+    if (starts[mid] < p) lo = mid + 1;
+    else hi = mid - 1;
+  }
+  return UINT_MAX;
+}
+
+}  // namespace ghostm

@@ -1,0 +1,63 @@
+// formats.h — readers for the formatted query and database files consumed by
+// `aln` (on-disk layout defined by the reference formatters):
+//   query  <p>.inf      {i32 division, u32 L, u32 max_nseq, 32 x i32 pad}   query_creator.cpp:327-346
+//          <p>_<i>.inf  {u32 nseq, u32 L}; .nam one name per line; .seq nseq*L codes
+//   db     <p>.inf      {i32 division, u32 seed, u32 maxlen, u64 sum_residues, pad}
+//          <p>_<i>.inf  {u32 nseq, u32 len}; .nam; .pos u32[nseq] subject starts;
+//          .seq u8[len] END-separated; .ind {u32 seed, u32 kcl, u32 npos,
+//          u32 keys_count[kcl] (CSR offsets), u32 positions[npos]}
+// Readers mirror QueryReader/Query (query_reader.cpp:34-102, query.cpp:37-79) and
+// DBReader/DB/Index (db_reader.cpp:34-77, db.cpp:36-123, index.h:86-126).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace ghostm {
+
+struct QueryChunk {
+  uint32_t id = 0;
+  uint32_t nseq = 0;
+  uint32_t L = 0;                  // fixed record width (X padded)
+  std::vector<std::string> names;  // one per record
+  std::vector<uint8_t> seq;        // nseq * L codes
+};
+
+struct QueryFile {
+  std::string prefix;
+  uint32_t division = 0, max_length = 0, max_nseq = 0;
+  explicit QueryFile(const std::string &prefix);
+  // Chunk `id` or false if id >= division / files missing.
+  bool ReadChunk(uint32_t id, QueryChunk *out) const;
+};
+
+struct DbChunk {
+  uint32_t id = 0;
+  uint32_t nseq = 0;
+  uint32_t len = 0;                // concatenated length incl. END separators
+  std::vector<std::string> names;
+  std::vector<uint32_t> starts;    // subject start offsets (.pos)
+  std::vector<uint8_t> seq;
+  uint32_t seed = 0, kcl = 0, npos = 0;
+  std::vector<uint32_t> keys_count;
+  std::vector<uint32_t> positions;
+  // Subject containing concatenated position p (DB::GetID, db.h:106-135).
+  uint32_t SubjectOf(uint32_t p) const;
+};
+
+struct DbFile {
+  std::string prefix;
+  int32_t division = 0;
+  uint32_t seed = 0, max_length = 0;
+  uint64_t sum_length = 0;
+  explicit DbFile(const std::string &prefix);
+  bool ReadChunk(uint32_t id, DbChunk *out) const;
+};
+
+// Seed helpers (Index::GetSeedLength / GetSeedWeight, index.h:116-141).
+uint32_t SeedLength(uint32_t seed);
+uint32_t SeedWeight(uint32_t seed);
+
+std::vector<std::string> ReadNameLines(const std::string &path, uint32_t n, bool *complete);
+
+}  // namespace ghostm

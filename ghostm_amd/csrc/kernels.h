@@ -1,0 +1,491 @@
+// kernels.h — gfx950 kernels of the `aln` hot path (included by device.hip only).
+//
+// K1 k_seed      one 512-thread workgroup per query. The query's k-mer position
+//                lists (62 at L=127) are gathered from the CSR index, turned into
+//                diagonal bins (one "dup" bit marks a repeat of the same bin inside
+//                one list), merged in LDS by a merge-path tree, and the run-length
+//                emission rule of SearchNextCpu is applied to the sorted bins.
+//                reference aligner.cpp:399-508; GPU twin aligner_gpu.cu:124-367.
+// K2 k_score     lane-group anti-diagonal Gotoh DP. A candidate is owned by a group
+//                of G lanes; lane i holds query rows [i*S, i*S+S) in registers and
+//                runs one DB column behind lane i-1, which hands it (H, F) of its
+//                last row through a wave shuffle each step. Per-query score
+//                profiles live in LDS. reference aligner.cpp:571-675.
+// K3 k_traceback the reverse DP of TraceBack with the same lane-group layout, the
+//                (match, length) bookkeeping packed into one int per row.
+//                reference aligner.cpp:800-947.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ghostm {
+namespace kern {
+
+constexpr uint32_t kSeqEnd = 25;
+constexpr uint32_t kPadCode = 31;      // unused residue code: query padding rows
+constexpr int kNeg = -30000;           // score of a padding row (keeps it at 0)
+
+// ------------------------------------------------------------------ K1 seed
+constexpr uint32_t kSeedBlock = 512;
+constexpr uint32_t kSeedLdsCap = 16384;   // bins per LDS buffer (2 buffers)
+constexpr uint32_t kMaxLists = 128;
+constexpr uint32_t kOverflow = 0xFFFFFFFFu;
+
+struct SeedArgs {
+  const uint8_t *qseq;
+  uint32_t L;
+  const uint32_t *keys_count;
+  const uint32_t *positions;
+  uint32_t seed_mask, nlists, shift, log_region, threshold;
+  const uint32_t *query_list;     // null: query = blockIdx.x
+  uint32_t *counts;               // [nq] candidates per query
+  uint32_t *nelem;                // [nq] bins of a query that did not fit LDS
+  uint32_t *slots;                // slot mode: candidates at q*slot_cap
+  uint32_t slot_cap;
+  const unsigned long long *offsets;  // offset mode: candidates at offsets[q]
+  uint32_t *out_start;
+  uint32_t *out_qid;
+  uint32_t *gbuf;                 // global merge buffers (GBUF variant)
+  const unsigned long long *gbuf_off;
+};
+
+__device__ inline uint32_t BlockExclusiveScan(uint32_t v, uint32_t *s_part, uint32_t *s_total) {
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  if (lane == 63) s_part[wid] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (uint32_t w = 0; w < blockDim.x / 64; ++w) {
+      const uint32_t t = s_part[w];
+      s_part[w] = acc;
+      acc += t;
+    }
+    *s_total = acc;
+  }
+  __syncthreads();
+  const uint32_t r = x - v + s_part[wid];
+  __syncthreads();
+  return r;
+}
+
+// Length of the run of `key` starting at i in sorted S[0..n).
+__device__ inline uint32_t RunLength(const uint32_t *S, uint32_t n, uint32_t i, uint32_t key) {
+  uint32_t k = i;
+  while (k < n && S[k] == key) ++k;
+  return k - i;
+}
+
+// Does the run head at i (non-dup key) satisfy c(b) + c(b+1) >= threshold?
+__device__ inline bool EmitRun(const uint32_t *S, uint32_t n, uint32_t i, uint32_t key,
+                               uint32_t threshold) {
+  const uint32_t c0 = RunLength(S, n, i, key);
+  uint32_t k = i + c0;
+  while (k < n && S[k] == (key | 1u)) ++k;
+  uint32_t c1 = 0;
+  if (k < n && S[k] == key + 2u) c1 = RunLength(S, n, k, key + 2u);
+  return c0 + c1 >= threshold;
+}
+
+template <bool GBUF>
+__global__ __launch_bounds__(kSeedBlock) void k_seed(SeedArgs a) {
+  __shared__ uint32_t s_beg[kMaxLists];
+  __shared__ uint32_t s_off[kMaxLists + 1];
+  __shared__ uint32_t s_part[kSeedBlock / 64];
+  __shared__ uint32_t s_total;
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_buf[];
+
+  const uint32_t item = blockIdx.x;
+  const uint32_t q = a.query_list ? a.query_list[item] : item;
+  const uint32_t tid = threadIdx.x;
+  const uint8_t *qs = a.qseq + (size_t)q * a.L;
+
+  // 1. one k-mer list per seed offset j*shift; drop positions before the offset
+  uint32_t len = 0;
+  if (tid < a.nlists) {
+    const uint32_t d0 = tid * a.shift;
+    uint32_t key = 0, t = 0;
+    for (uint32_t s = a.seed_mask; s; s >>= 1, ++t)
+      if (s & 1u) key = (key << 5) | qs[d0 + t];
+    const uint32_t b = a.keys_count[key], e = a.keys_count[key + 1];
+    uint32_t lo = b, hi = e;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (a.positions[mid] < d0) lo = mid + 1; else hi = mid;
+    }
+    s_beg[tid] = lo;
+    len = e - lo;
+  }
+  const uint32_t excl = BlockExclusiveScan(len, s_part, &s_total);
+  if (tid < a.nlists) s_off[tid] = excl;
+  if (tid == 0) s_off[a.nlists] = s_total;
+  __syncthreads();
+  const uint32_t n = s_off[a.nlists];
+  if (n == 0) {
+    if (tid == 0) a.counts[q] = 0;
+    return;
+  }
+  uint32_t *buf0, *buf1;
+  if (GBUF) {
+    buf0 = a.gbuf + a.gbuf_off[item];
+    buf1 = buf0 + n;
+  } else {
+    if (n > kSeedLdsCap) {
+      if (tid == 0) { a.counts[q] = kOverflow; a.nelem[q] = n; }
+      return;
+    }
+    buf0 = s_buf;
+    buf1 = s_buf + kSeedLdsCap;
+  }
+
+  // 2. gather: key = bin << 1 | (bin repeats the previous bin of the same list)
+  const uint32_t nl = a.nlists;
+  for (uint32_t i = tid; i < n; i += kSeedBlock) {
+    uint32_t lo = 0, hi = nl - 1;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      if (s_off[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    const uint32_t r = i - s_off[lo], idx = s_beg[lo] + r, d0 = lo * a.shift;
+    const uint32_t bin = (a.positions[idx] - d0) >> a.log_region;
+    uint32_t dup = 0;
+    if (r > 0) dup = ((a.positions[idx - 1] - d0) >> a.log_region) == bin;
+    buf0[i] = (bin << 1) | dup;
+  }
+
+  // 3. merge-path tree: segments of w lists are merged pairwise per round
+  uint32_t *src = buf0, *dst = buf1;
+  const uint32_t per = (n + kSeedBlock - 1) / kSeedBlock;
+  for (uint32_t w = 1; w < nl; w <<= 1) {
+    __syncthreads();
+    const uint32_t npairs = (nl + 2 * w - 1) / (2 * w);
+    uint32_t g = min(n, tid * per);
+    const uint32_t gend = min(n, g + per);
+    while (g < gend) {
+      uint32_t lo = 0, hi = npairs - 1;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (s_off[min(2 * mid * w, nl)] <= g) lo = mid; else hi = mid - 1;
+      }
+      const uint32_t P0 = s_off[min(2 * lo * w, nl)];
+      const uint32_t P1 = s_off[min((2 * lo + 1) * w, nl)];
+      const uint32_t P2 = s_off[min((2 * lo + 2) * w, nl)];
+      const uint32_t *A = src + P0, *B = src + P1;
+      const uint32_t na = P1 - P0, nb = P2 - P1;
+      const uint32_t d0 = g - P0, d1 = min(gend, P2) - P0;
+      uint32_t l2 = d0 > nb ? d0 - nb : 0, h2 = min(d0, na);
+      while (l2 < h2) {
+        const uint32_t mid = (l2 + h2) >> 1;
+        if (A[mid] <= B[d0 - 1 - mid]) l2 = mid + 1; else h2 = mid;
+      }
+      uint32_t ia = l2, ib = d0 - l2;
+      for (uint32_t d = d0; d < d1; ++d) {
+        uint32_t v;
+        if (ib >= nb || (ia < na && A[ia] <= B[ib])) v = A[ia++]; else v = B[ib++];
+        dst[P0 + d] = v;
+      }
+      g = P0 + d1;
+    }
+    uint32_t *t = src; src = dst; dst = t;
+  }
+  __syncthreads();
+
+  // 4. emission: bin b (first non-dup key of its run) if c(b)+c(b+1) >= t, in
+  //    ascending order; the phantom bin 0 precedes everything when b=1 is the
+  //    smallest bin (the reference's initial state distance=0, count=0).
+  const uint32_t *S = src;
+  const uint32_t g0 = min(n, tid * per), g1 = min(n, g0 + per);
+  const uint32_t thr = a.threshold;
+  uint32_t mine = 0;
+  bool phantom = false;
+  if (thr != 0) {
+    if (tid == 0 && S[0] == 2u && RunLength(S, n, 0, 2u) >= thr) phantom = true;
+    for (uint32_t i = g0; i < g1; ++i) {
+      const uint32_t key = S[i];
+      if ((key & 1u) || (i > 0 && S[i - 1] == key)) continue;
+      if (EmitRun(S, n, i, key, thr)) ++mine;
+    }
+  }
+  mine += phantom ? 1u : 0u;
+  const uint32_t base = BlockExclusiveScan(mine, s_part, &s_total);
+  const uint32_t total = s_total;
+  if (tid == 0) a.counts[q] = total;
+  uint32_t *os = nullptr, *oq = nullptr;
+  if (a.offsets) {
+    os = a.out_start + a.offsets[q];
+    oq = a.out_qid + a.offsets[q];
+  } else if (a.slots && total <= a.slot_cap) {
+    os = a.slots + (size_t)q * a.slot_cap;
+  }
+  if (!os || mine == 0) return;
+  uint32_t at = base;
+  if (phantom) {
+    os[at] = 0;
+    if (oq) oq[at] = q;
+    ++at;
+  }
+  for (uint32_t i = g0; i < g1; ++i) {
+    const uint32_t key = S[i];
+    if ((key & 1u) || (i > 0 && S[i - 1] == key)) continue;
+    if (EmitRun(S, n, i, key, thr)) {
+      os[at] = (key >> 1) << a.log_region;
+      if (oq) oq[at] = q;
+      ++at;
+    }
+  }
+}
+
+// Slot -> compact copy for queries whose candidates fit their slot.
+__global__ void k_compact(const uint32_t *slots, uint32_t slot_cap, const uint32_t *counts,
+                          const uint32_t *nelem, const unsigned long long *offsets,
+                          uint32_t nq, uint32_t *out_start, uint32_t *out_qid) {
+  const uint32_t q = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (q >= nq) return;
+  const uint32_t c = counts[q];
+  if (nelem[q] != 0 || c > slot_cap) return;
+  const unsigned long long o = offsets[q];
+  for (uint32_t i = threadIdx.x & 63; i < c; i += 64) {
+    out_start[o + i] = slots[(size_t)q * slot_cap + i];
+    out_qid[o + i] = q;
+  }
+}
+
+// ------------------------------------------------------------------ K2 score
+constexpr int kScoreBlock = 256;
+constexpr int kScoreQmax = 4;
+constexpr uint32_t kProfRows = 26;
+
+struct ScoreTask {
+  unsigned long long begin;  // first candidate (global index)
+  uint32_t count;            // candidates in this task
+  uint32_t q_first;          // first query of the task (profile slot 0)
+  uint32_t q_count;          // profile slots used
+  uint32_t pad;
+};
+
+struct ScoreArgs {
+  const uint8_t *qseq;
+  uint32_t L, Lpad, pad, G, gpw;
+  const uint8_t *db;
+  uint32_t dblen;
+  const int *mat;            // 32x32, column 31 = kNeg
+  const uint32_t *cand_qid;
+  const uint32_t *cand_start;
+  const ScoreTask *tasks;
+  uint32_t base, extend;
+  int open, ext;
+  uint32_t *score_out;
+  uint32_t *end_out;
+  unsigned long long out_base;
+};
+
+template <int S>
+__global__ __launch_bounds__(kScoreBlock) void k_score(ScoreArgs a) {
+  extern __shared__ __attribute__((aligned(16))) int s_prof[];
+  const ScoreTask t = a.tasks[blockIdx.x];
+  const uint32_t RS = a.Lpad + 4;  // padded profile row (spreads LDS banks)
+
+  // per-query profiles: prof[slot][c][r] = M[c][q[r - pad]], padding rows kNeg.
+  // Rows 0..24 are the residue codes; row 25 stands for codes 26..31, whose
+  // matrix rows are all zero (the reader only fills codes <= 24).
+  const uint32_t per_slot = kProfRows * a.Lpad;
+  const uint32_t total = t.q_count * per_slot;
+  for (uint32_t e = threadIdx.x; e < total; e += kScoreBlock) {
+    const uint32_t slot = e / per_slot, rem = e - slot * per_slot;
+    const uint32_t c = rem / a.Lpad, r = rem - c * a.Lpad;
+    int v = kNeg;
+    if (r >= a.pad) v = c < 25 ? a.mat[c * 32 + a.qseq[(size_t)(t.q_first + slot) * a.L + (r - a.pad)]] : 0;
+    s_prof[(slot * kProfRows + c) * RS + r] = v;
+  }
+  __syncthreads();
+
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t g = lane / a.G, i = lane - g * a.G;
+  const uint32_t local = wave * a.gpw + g;
+  const bool valid = g < a.gpw && local < t.count;
+  const unsigned long long cand = t.begin + local;
+  uint32_t slot = 0, off = 0, width = 0;
+  if (valid) {
+    slot = a.cand_qid[cand] - t.q_first;
+    int o = (int)(a.cand_start[cand] - a.extend);
+    if (o < 0) o = 0;
+    off = (uint32_t)o;
+    width = a.base;
+    if (off + width > a.dblen) width = a.dblen - off;
+  }
+  const int *prof = s_prof + slot * kProfRows * RS + i * S;
+
+  int H[S], E[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) { H[k] = 0; E[k] = 0; }
+  int best = 0, best_col = 0;
+  int hout = 0, fout = 0, hprev = 0;
+  const int open = a.open, ext = a.ext;
+  int j = -(int)i;
+  uint32_t cnext = 0;
+  if (valid && j >= 0 && (uint32_t)j < width) cnext = a.db[off + j];
+  const uint32_t steps = a.base + a.G - 1;
+  for (uint32_t step = 0; step < steps; ++step, ++j) {
+    int hin = __shfl_up(hout, 1), fin = __shfl_up(fout, 1);
+    if (i == 0) { hin = 0; fin = 0; }
+    const int diag0 = hprev;
+    hprev = hin;
+    const bool active = valid && j >= 0 && (uint32_t)j < width;
+    const uint32_t c = cnext;
+    if (valid && j + 1 >= 0 && (uint32_t)(j + 1) < width) cnext = a.db[off + j + 1];
+    hout = 0;
+    fout = 0;
+    if (active) {
+      if (c == kSeqEnd) {
+#pragma unroll
+        for (int k = 0; k < S; ++k) { H[k] = 0; E[k] = 0; }
+      } else {
+        const int *p = prof + (c < 25 ? c : 25u) * RS;
+        int diag = diag0, F = fin, cm = 0;
+#pragma unroll
+        for (int k = 0; k < S; k += 4) {
+          const int4 pv = *reinterpret_cast<const int4 *>(p + k);
+          const int pk[4] = {pv.x, pv.y, pv.z, pv.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int s = diag + pk[u];
+            const int h = max(max(s, E[k + u]), F);
+            diag = H[k + u];
+            H[k + u] = h;
+            const int o = h + open;
+            E[k + u] = max(max(E[k + u] + ext, o), 0);
+            F = max(max(F + ext, o), 0);
+            cm = max(cm, h);
+          }
+        }
+        hout = H[S - 1];
+        fout = F;
+        if (cm >= best) { best = cm; best_col = j; }
+      }
+    }
+  }
+  // combine the strips of a group: max score, then the last column reaching it
+  int B = best, C = best_col;
+  for (uint32_t k = 1; k < a.G; ++k) {
+    const int ob = __shfl(best, g * a.G + k), oc = __shfl(best_col, g * a.G + k);
+    if (ob > B || (ob == B && oc > C)) { B = ob; C = oc; }
+  }
+  if (valid && i == 0) {
+    a.score_out[cand - a.out_base] = (uint32_t)B;
+    a.end_out[cand - a.out_base] = off + (uint32_t)C;
+  }
+}
+
+// ------------------------------------------------------------------ K3 traceback
+constexpr int kTbBlock = 256;
+
+struct TbArgs {
+  const uint8_t *qseq;
+  uint32_t L, Lpad, G, gpw;
+  const uint8_t *db;
+  const int *mat_tb;          // (score << 16) | (0x100 | eq), column 31 = kNeg << 16
+  const uint32_t *qid;
+  const uint32_t *end;
+  uint32_t n;
+  uint32_t base;
+  int open, ext;
+  uint32_t *out_start;
+  uint32_t *out_ml;           // (aln_len << 8) | matches
+};
+
+template <int S>
+__global__ __launch_bounds__(kTbBlock) void k_traceback(TbArgs a) {
+  __shared__ int s_mat[32 * 32];
+  for (uint32_t e = threadIdx.x; e < 32 * 32; e += kTbBlock) s_mat[e] = a.mat_tb[e];
+  __syncthreads();
+
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t g = lane / a.G, i = lane - g * a.G;
+  const uint32_t hit = (blockIdx.x * (kTbBlock / 64) + wave) * a.gpw + g;
+  const bool valid = g < a.gpw && hit < a.n;
+  uint32_t p0 = 0, width = 0;
+  // processing row U = i*S + u walks the query backwards: position L-1-(U-pad)
+  uint32_t qcode[S / 4];
+#pragma unroll
+  for (int w = 0; w < S / 4; ++w) qcode[w] = 0x1F1F1F1Fu;
+  if (valid) {
+    p0 = a.end[hit];
+    width = p0 < a.base ? p0 + 1 : a.base;
+    const uint8_t *qs = a.qseq + (size_t)a.qid[hit] * a.L;
+#pragma unroll
+    for (int u = 0; u < S; ++u) {
+      const int k = (int)a.Lpad - 1 - (int)(i * S + u);
+      const uint32_t code = (k >= 0 && k < (int)a.L) ? qs[k] : kPadCode;
+      qcode[u >> 2] = (qcode[u >> 2] & ~(0xFFu << (8 * (u & 3)))) | (code << (8 * (u & 3)));
+    }
+  }
+  int H[S], E[S], M[S];
+#pragma unroll
+  for (int u = 0; u < S; ++u) { H[u] = 0; E[u] = 0; M[u] = 0; }
+  int best = 0, best_col = 0, best_ml = 0;
+  int hout = 0, fout = 0, mout = 0, hprev = 0, mprev = 0;
+  bool done = false;
+  const int open = a.open, ext = a.ext;
+  int j = -(int)i;
+  const uint32_t steps = a.base + a.G - 1;
+  for (uint32_t step = 0; step < steps; ++step, ++j) {
+    int hin = __shfl_up(hout, 1), fin = __shfl_up(fout, 1), min_ = __shfl_up(mout, 1);
+    if (i == 0) { hin = 0; fin = 0; min_ = 0; }
+    const int diag0 = hprev, tml0 = mprev;
+    hprev = hin;
+    mprev = min_;
+    bool active = valid && !done && j >= 0 && (uint32_t)j < width;
+    uint32_t c = 0;
+    if (active) {
+      c = a.db[p0 - j];
+      if (c == kSeqEnd) { done = true; active = false; }
+    }
+    if (active) {
+      const int *row = s_mat + c * 32;
+      int diag = diag0, tml = tml0, F = fin, hup = hin, mup = min_;
+#pragma unroll
+      for (int u = 0; u < S; ++u) {
+        const int P = row[(qcode[u >> 2] >> (8 * (u & 3))) & 0xFFu];
+        const int s = diag + (P >> 16);
+        int h = 0, ml = 0;
+        if (s > 0) { h = s; ml = tml + (P & 0xFFFF); }
+        const int e = max(E[u] + ext, H[u] + open);
+        E[u] = e;
+        if (e > h) { h = e; ml = M[u] + 0x100; }
+        F = max(F + ext, hup + open);
+        if (F > h) { h = F; ml = mup + 0x100; }
+        diag = H[u];
+        tml = M[u];
+        H[u] = h;
+        M[u] = ml;
+        hup = h;
+        mup = ml;
+        if (h > best) { best = h; best_col = j; best_ml = ml; }
+      }
+      hout = H[S - 1];
+      fout = F;
+      mout = M[S - 1];
+    } else {
+      hout = 0; fout = 0; mout = 0;
+    }
+  }
+  // first cell (column-major, rows in processing order) reaching the maximum
+  int B = best, C = best_col, ML = best_ml;
+  for (uint32_t k = 1; k < a.G; ++k) {
+    const int src = (int)(g * a.G + k);
+    const int ob = __shfl(best, src), oc = __shfl(best_col, src), om = __shfl(best_ml, src);
+    if (ob > B || (ob == B && ob > 0 && oc < C)) { B = ob; C = oc; ML = om; }
+  }
+  if (valid && i == 0) {
+    a.out_start[hit] = p0 - (uint32_t)C;
+    a.out_ml[hit] = (uint32_t)ML;
+  }
+}
+
+}  // namespace kern
+}  // namespace ghostm

@@ -1,0 +1,136 @@
+"""ctypes binding of the C ABI in include/ghostm_hip.h (libghostm_hip.so).
+
+The library is built in-tree (ghostm_amd/lib) by `__graft_entry__.build()` /
+`make -C ghostm_amd/csrc`. There is no fallback: if the library is missing or a
+symbol is absent, loading raises, so nothing silently runs on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+from ctypes import POINTER, c_char_p, c_float, c_int, c_size_t, c_uint32, c_uint64, c_void_p
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libghostm_hip.so")
+BIN_PATH = os.path.join(PKG_DIR, "bin", "ghostm")
+HEADER_PATH = os.path.join(REPO_DIR, "include", "ghostm_hip.h")
+
+u32p = POINTER(c_uint32)
+
+
+class GhostmHit(ctypes.Structure):
+    """reference Alignment fields gathered per hit (alignment.h:136-145)."""
+
+    _fields_ = [
+        ("query_id", c_uint32),
+        ("db_id", c_uint32),
+        ("score", c_uint32),
+        ("db_start", c_uint32),
+        ("db_end", c_uint32),
+        ("aln_len", c_uint32),
+        ("aln_match", c_uint32),
+        ("seq_id", c_float),
+    ]
+
+
+class GhostmStats(ctypes.Structure):
+    _fields_ = [
+        ("seconds_total", ctypes.c_double),
+        ("seconds_seed", ctypes.c_double),
+        ("seconds_score", ctypes.c_double),
+        ("seconds_traceback", ctypes.c_double),
+        ("seconds_merge", ctypes.c_double),
+        ("seconds_output", ctypes.c_double),
+        ("queries", c_uint64),
+        ("query_residues", c_uint64),
+        ("candidates", c_uint64),
+        ("score_cells", c_uint64),
+        ("tracebacks", c_uint64),
+        ("traceback_cells", c_uint64),
+        ("hits", c_uint64),
+        ("batches", c_uint64),
+        ("score_launches", c_uint64),
+        ("seed_bytes", c_uint64),
+    ]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+# name -> (restype, argtypes); covers every function declared in the header
+SIGNATURES = {
+    "InitGpu": (c_int, []),
+    "GetNeededGPUMemorySize": (c_size_t, [c_uint32] * 6),
+    "CheckGpuMemory": (c_int, [c_uint32] * 6),
+    "SetOptionGpu": (c_int, [c_uint32, POINTER(c_int), c_int]),
+    "printGpuInfo": (None, [c_int]),
+    "SetQueryGpu": (c_int, [POINTER(ctypes.c_uint8), c_uint32, c_uint32]),
+    "SetDbGpu": (c_int, [POINTER(ctypes.c_uint8), c_uint32, u32p, c_uint32, u32p, c_uint32]),
+    "SearchNextGpu": (c_uint32, [c_uint32] * 8 + [u32p, u32p]),
+    "CalculateScoreGpu": (None, [c_uint32, c_uint32, c_uint32, u32p, u32p, c_uint32, c_uint32, c_int, c_int]),
+    "FreeGpu": (c_int, []),
+    "GhostmGetLastError": (c_char_p, []),
+    "GhostmBuildInfo": (c_char_p, []),
+    "CountCandidatesGpu": (c_int, [c_uint32] * 6 + [u32p]),
+    "TraceBackGpu": (c_int, [c_uint32, u32p, u32p, c_uint32, c_uint32, c_int, c_int, u32p, u32p, u32p, POINTER(c_float)]),
+    "GhostmSessionCreate": (c_void_p, [c_int, POINTER(c_char_p)]),
+    "GhostmSessionRun": (c_int, [c_void_p]),
+    "GhostmSessionOutput": (c_size_t, [c_void_p, c_char_p, c_size_t]),
+    "GhostmSessionWrite": (c_int, [c_void_p]),
+    "GhostmSessionHits": (c_size_t, [c_void_p, POINTER(GhostmHit), c_size_t]),
+    "GhostmSessionStats": (c_int, [c_void_p, POINTER(GhostmStats)]),
+    "GhostmSessionDestroy": (None, [c_void_p]),
+    "GhostmAlignMain": (c_int, [c_int, POINTER(c_char_p)]),
+}
+
+_lib = None
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def header_functions(path: str = HEADER_PATH) -> list[str]:
+    """Function names declared in include/ghostm_hip.h."""
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\(", text)
+    skip = {"if", "defined", "sizeof"}
+    out = []
+    for n in names:
+        if n in skip or n in out:
+            continue
+        out.append(n)
+    return out
+
+
+def load() -> ctypes.CDLL:
+    """Load libghostm_hip.so (raises NativeLibraryMissing if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeLibraryMissing(
+            f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+        )
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)  # AttributeError if the symbol is missing
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    return (load().GhostmGetLastError() or b"").decode(errors="replace")
+
+
+def argv_array(args: list[str]):
+    arr = (c_char_p * (len(args) + 1))()
+    for i, a in enumerate(args):
+        arr[i] = a.encode()
+    arr[len(args)] = None
+    return arr

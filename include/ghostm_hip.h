@@ -1,0 +1,173 @@
+/*
+ * ghostm_hip.h — C ABI of the MI355X (gfx950) search/align plugin.
+ *
+ * Part 1 is the reference GPU plugin surface, symbol for symbol: GHOSTM 2.0's
+ * aligner.cpp binds exactly these ten functions (reference aligner_gpu.h:33-114,
+ * called from aligner.cpp:77-93, 110, 123-124, 356-361, 529-531, 211). A build of
+ * the reference host that links libghostm_hip.so instead of aligner_gpu.o runs
+ * its `-D <device>` path on this implementation unchanged.
+ *
+ * Part 2 extends the surface where the reference ABI cannot express the whole
+ * hot path: a whole-query-set candidate count (needed to
+ * reproduce the CPU path's batching exactly), a device traceback, error strings
+ * instead of exit(), and a session API that runs the complete `aln` pipeline
+ * (seed -> score -> merge -> traceback -> E-value) with inputs resident in HBM.
+ *
+ * Conventions: plain pointers and sizes, no C++ or torch types. Host arrays are
+ * owned by the caller; copies are synchronous unless stated. Int returns: 0 = OK,
+ * non-zero = error (message via GhostmGetLastError). One device per process.
+ */
+#ifndef GHOSTM_HIP_H_
+#define GHOSTM_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------- Part 1: reference plugin surface ------------------------ */
+
+/* replaces aligner_gpu.h:37 InitGpu (aligner_gpu.cu:588) — reset module state */
+int InitGpu(void);
+
+/* replaces aligner_gpu.h:39-47 (aligner_gpu.cu:506) — device bytes the search
+ * needs for the given maxima (counts this build's buffers, not the reference's) */
+size_t GetNeededGPUMemorySize(uint32_t seed, uint32_t shift_size,
+                              uint32_t max_list_length, uint32_t max_query_length,
+                              uint32_t max_number_queries, uint32_t max_db_length);
+
+/* replaces aligner_gpu.h:49-57 (aligner_gpu.cu:560) — 1 if it does not fit */
+int CheckGpuMemory(uint32_t seed, uint32_t shift_size, uint32_t max_list_length,
+                   uint32_t max_query_length, uint32_t max_number_queries,
+                   uint32_t max_db_length);
+
+/* replaces aligner_gpu.h:59-64 (aligner_gpu.cu:620) — bind device, upload the
+ * 32x32 score matrix M[db_code*32 + query_code], size candidate buffers */
+int SetOptionGpu(uint32_t max_list_length, int score_matrix[], int device);
+
+/* replaces aligner_gpu.h:66 (aligner_gpu.cu:646) */
+void printGpuInfo(int device);
+
+/* replaces aligner_gpu.h:68-73 (aligner_gpu.cu:654) — upload a query chunk of
+ * number_sequences fixed-width records of sequence_length codes */
+int SetQueryGpu(uint8_t sequences[], uint32_t number_sequences, uint32_t sequence_length);
+
+/* replaces aligner_gpu.h:75-83 (aligner_gpu.cu:691) — upload a DB chunk and its
+ * k-mer index (keys_count = CSR offsets, positions = ascending per key) */
+int SetDbGpu(uint8_t sequences[], uint32_t sequences_legnth, uint32_t keys_count[],
+             uint32_t keys_count_length, uint32_t positions[], uint32_t positions_length);
+
+/* replaces aligner_gpu.h:85-97 (aligner_gpu.cu:759) — seed search for the queries
+ * from start_query_id on. Batches queries with the reference GPU rule (stop before
+ * the running candidate total reaches max_number_alignments). Fills
+ * alignment_count_list[0..q] (prefix counts) and starts[] (candidate DB starts,
+ * ascending per query); returns q = number of queries in the batch. The starts
+ * stay resident on the device for the next CalculateScoreGpu. */
+uint32_t SearchNextGpu(uint32_t query_sequence_length, uint32_t number_query_sequences,
+                       uint32_t seed, uint32_t threshold, uint32_t shift_size,
+                       uint32_t log_region_size, uint32_t max_number_alignments,
+                       uint32_t start_query_id, uint32_t *alignment_count_list,
+                       uint32_t *starts);
+
+/* replaces aligner_gpu.h:99-110 (aligner_gpu.cu:971) — Gotoh local score + end of
+ * every candidate of the last SearchNextGpu batch */
+void CalculateScoreGpu(uint32_t db_length, uint32_t query_sequence_length,
+                       uint32_t number_alignment_list, uint32_t scores[], uint32_t ends[],
+                       uint32_t base_search_length, uint32_t offset, int open_gap,
+                       int extend_gap);
+
+/* replaces aligner_gpu.h:112 (aligner_gpu.cu:1029) */
+int FreeGpu(void);
+
+/* ---------------- Part 2: extensions -------------------------------------- */
+
+/* Last error message of this thread's most recent failing call ("" if none). */
+const char *GhostmGetLastError(void);
+
+/* Build identity (kernel variant names, arch), for logs. */
+const char *GhostmBuildInfo(void);
+
+/* Candidate count of EVERY query of the resident chunk (no batching), K1 count
+ * pass; counts[number_query_sequences]. Lets a host reproduce the CPU path's
+ * batch cuts exactly (reference aligner.cpp:511-514). */
+int CountCandidatesGpu(uint32_t query_sequence_length, uint32_t number_query_sequences,
+                       uint32_t seed, uint32_t threshold, uint32_t shift_size,
+                       uint32_t log_region_size, uint32_t counts[]);
+
+/* Reverse-DP traceback (reference aligner.cpp:771-949) of nhits hits on the
+ * resident query/DB chunk: per hit (query_id, db_end) -> db_start (absolute),
+ * aln_len, aln_match, seq_id = match/len (float). base_search_length is the
+ * reference's L + 2*e*2*R window. */
+int TraceBackGpu(uint32_t nhits, const uint32_t query_ids[], const uint32_t db_ends[],
+                 uint32_t query_sequence_length, uint32_t base_search_length,
+                 int open_gap, int extend_gap, uint32_t db_starts[], uint32_t aln_lens[],
+                 uint32_t aln_matches[], float seq_ids[]);
+
+/* One resolved hit, the record gathered across ranks (32 bytes). Coordinates are
+ * subject-relative, as printed minus one. */
+typedef struct GhostmHit {
+  uint32_t query_id;   /* global query index over all chunks */
+  uint32_t db_id;      /* global subject index over all DB chunks */
+  uint32_t score;
+  uint32_t db_start;
+  uint32_t db_end;
+  uint32_t aln_len;
+  uint32_t aln_match;
+  float seq_id;
+} GhostmHit;
+
+/* Stage timings / work counters of the last GhostmSessionRun. */
+typedef struct GhostmStats {
+  double seconds_total;      /* whole run, host wall clock */
+  double seconds_seed;       /* K1 count + write passes (device time) */
+  double seconds_score;      /* K2 (device time) */
+  double seconds_traceback;  /* K3 (device time) */
+  double seconds_merge;      /* host Merge (sort/dedup/select) */
+  double seconds_output;     /* host E-value + text formatting */
+  uint64_t queries;
+  uint64_t query_residues;   /* sum over queries of non-X prefix length */
+  uint64_t candidates;
+  uint64_t score_cells;      /* sum over candidates of L x non-END window columns */
+  uint64_t tracebacks;
+  uint64_t traceback_cells;
+  uint64_t hits;
+  uint64_t batches;
+  uint64_t score_launches;
+  uint64_t seed_bytes;       /* algorithmic bytes of the K1 passes */
+} GhostmStats;
+
+/* Session: parse `aln` options exactly like the reference (getopt string
+ * "b:d:D:e:E:G:i:l:M:o:r:s:t:S:L:y:v", aligner.cpp:225-345; argv[0] is ignored),
+ * load every query and DB chunk and make them resident on the device given by
+ * -D (default 0). Returns NULL on error. */
+void *GhostmSessionCreate(int argc, char **argv);
+
+/* Run the whole search with the CPU path's semantics (batch cuts, merge order,
+ * tie rules) on the device. Results replace those of any previous run. */
+int GhostmSessionRun(void *session);
+
+/* Formatted output of the last run (reference WriteOutput/V1/V2 text). With
+ * buf == NULL returns the byte count; otherwise copies min(cap, size) bytes. */
+size_t GhostmSessionOutput(void *session, char *buf, size_t cap);
+
+/* Write the formatted output of the last run to the -o file. */
+int GhostmSessionWrite(void *session);
+
+/* Hit records of the last run in output order; same NULL/cap convention. */
+size_t GhostmSessionHits(void *session, GhostmHit *hits, size_t cap);
+
+int GhostmSessionStats(void *session, GhostmStats *stats);
+
+void GhostmSessionDestroy(void *session);
+
+/* `ghostm aln ...` end to end (create + run + write + destroy). Exit status like
+ * the reference CLI: errors are printed and 0 is still returned (main.cpp:116-121). */
+int GhostmAlignMain(int argc, char **argv);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GHOSTM_HIP_H_ */

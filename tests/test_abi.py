@@ -1,0 +1,67 @@
+"""The C-ABI library loads on a CPU-only host and exports every function declared in
+include/ghostm_hip.h (no device calls here)."""
+import ctypes
+import os
+import subprocess
+
+import cases
+from ghostm_amd import native
+
+
+def test_library_exports_header_functions(built):
+    lib = native.load()
+    declared = native.header_functions()
+    assert len(declared) >= 22
+    for name in declared:
+        assert hasattr(lib, name), name
+        assert name in native.SIGNATURES, f"{name} has no ctypes signature"
+
+
+def test_reference_plugin_surface_present(built):
+    """The ten symbols the reference's aligner.cpp binds (aligner_gpu.h:33-114)."""
+    ref = ["InitGpu", "GetNeededGPUMemorySize", "CheckGpuMemory", "SetOptionGpu", "printGpuInfo",
+           "SetQueryGpu", "SetDbGpu", "SearchNextGpu", "CalculateScoreGpu", "FreeGpu"]
+    out = subprocess.run(["nm", "-D", "--defined-only", native.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    for s in ref:
+        assert s in exported, s
+
+
+def test_hit_record_layout():
+    assert ctypes.sizeof(native.GhostmHit) == 32
+    from ghostm_amd.aligner import HIT_DTYPE
+
+    assert HIT_DTYPE.itemsize == 32
+
+
+def test_reference_host_links_against_plugin():
+    """Where the reference was compiled here, its binary resolves the ten plugin
+    symbols from libghostm_hip.so (drop-in at the symbol level)."""
+    if not os.path.exists(cases.REF):
+        import pytest
+
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    out = subprocess.run(["ldd", cases.REF], capture_output=True, text=True, check=True).stdout
+    assert "libghostm_hip.so" in out
+    und = subprocess.run(["nm", "-D", "--undefined-only", cases.REF], capture_output=True,
+                         text=True, check=True).stdout
+    for s in ["SearchNextGpu", "CalculateScoreGpu", "SetDbGpu", "SetQueryGpu"]:
+        assert s in und
+
+
+def test_cli_usage_and_unknown_command(built):
+    r = subprocess.run([cases.GHOSTM], capture_output=True)
+    assert r.returncode == 1
+    r = subprocess.run([cases.GHOSTM, "nope"], capture_output=True)
+    assert r.returncode == 1 and b"unrecognized command" in r.stderr
+
+
+def test_unsupported_score_option_exits_zero(tmp_path, built):
+    """statistics.cpp:143-145 + main.cpp:116-121: -y 0 with an unknown matrix/gap
+    combination prints the error, writes nothing, exits 0 (no device touched)."""
+    r = subprocess.run([cases.GHOSTM, "aln", "-i", "x", "-d", "y", "-o", str(tmp_path / "o"),
+                        "-G", "5"], capture_output=True)
+    assert r.returncode == 0
+    assert b"not support score option" in r.stderr
+    assert not (tmp_path / "o").exists()

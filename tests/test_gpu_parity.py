@@ -1,0 +1,178 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the reference
+golden outputs. Bit-exact text for every dataset/option variant; stage-level checks
+of the reference plugin surface (SearchNextGpu / CalculateScoreGpu / TraceBackGpu)
+against the oracle's stage dumps."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import cases
+from ghostm_amd import native
+from ghostm_amd.aligner import Session
+
+pytestmark = pytest.mark.gpu
+
+
+def _gpu_text(d, opts, env, out):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        with Session(["-i", os.path.join(d, "q"), "-d", os.path.join(d, "db"), "-o", out, "-D", "0"]
+                     + list(opts)) as s:
+            s.run()
+            text = s.output()
+            st = s.stats()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    return text, st
+
+
+@pytest.mark.parametrize("ds,var,opts,env", cases.VARIANTS, ids=[f"{v[0]}/{v[1]}" for v in cases.VARIANTS])
+def test_gpu_matches_reference_golden(ds, var, opts, env, dataset, golden, tmp_path):
+    d = dataset(ds)
+    text, st = _gpu_text(d, opts, env, str(tmp_path / "g.out"))
+    want = golden["aln"][f"{ds}/{var}"]
+    (tmp_path / "g.out").write_bytes(text)
+    assert text.count(b"\n") == want["lines"]
+    assert cases.sha256(str(tmp_path / "g.out")) == want["sha256"]
+
+
+@pytest.mark.parametrize("ds,var,opts,env", cases.BATCH_VARIANTS,
+                         ids=[f"{v[0]}/{v[1]}" for v in cases.BATCH_VARIANTS])
+def test_gpu_batch_cuts_match_oracle(ds, var, opts, env, dataset, tmp_path):
+    """CPU-path batch semantics (carry, drop of a carried last query, stop at the
+    first empty batch) at tiny -l, against the oracle."""
+    d = dataset(ds)
+    text, st = _gpu_text(d, opts, env, str(tmp_path / "g.out"))
+    want = cases.run_aln(cases.ORACLE, d, opts, env, str(tmp_path / "o.out"))
+    assert text == want
+    if env.get("GHOSTM_MAX_LIST_OVERRIDE") not in ("1",):
+        assert st["batches"] > 1
+
+
+def test_cli_aln_writes_same_file(dataset, golden, tmp_path):
+    d = dataset("syn_small")
+    out = tmp_path / "cli.out"
+    cases.run_aln(cases.GHOSTM, d, ["-D", "0"], {}, str(out))
+    assert cases.sha256(str(out)) == golden["aln"]["syn_small/default"]["sha256"]
+
+
+def test_session_rerun_is_identical(dataset, tmp_path):
+    d = dataset("syn_small")
+    with Session(["-i", f"{d}/q", "-d", f"{d}/db", "-o", str(tmp_path / "x"), "-D", "0"]) as s:
+        s.run()
+        a, ha = s.output(), s.hits()
+        s.run()
+        b, hb = s.output(), s.hits()
+    assert a == b and np.array_equal(ha, hb)
+    assert len(ha) == a.count(b"\n")
+
+
+# ------------------------------------------------------------ stage level
+def _load_chunk(d, qprefix="q", dprefix="db"):
+    inf = np.fromfile(f"{d}/{qprefix}_0.inf", dtype="<u4")
+    nq, L = int(inf[0]), int(inf[1])
+    qseq = np.fromfile(f"{d}/{qprefix}_0.seq", dtype=np.uint8)
+    dinf = np.fromfile(f"{d}/{dprefix}_0.inf", dtype="<u4")
+    dbseq = np.fromfile(f"{d}/{dprefix}_0.seq", dtype=np.uint8)
+    raw = np.fromfile(f"{d}/{dprefix}_0.ind", dtype="<u4")
+    seed, kcl, npos = (int(x) for x in raw[:3])
+    kc = np.ascontiguousarray(raw[3:3 + kcl])
+    pos = np.ascontiguousarray(raw[3 + kcl:3 + kcl + npos])
+    assert len(dbseq) == int(dinf[1])
+    return nq, L, qseq, dbseq, seed, kc, pos
+
+
+def _p(a, t=ctypes.c_uint32):
+    return a.ctypes.data_as(ctypes.POINTER(t))
+
+
+def _blosum62():
+    return cases.parse_ncbi_matrix(os.path.join(cases.GOLDEN, "matrices", "BLOSUM62"))
+
+
+def test_reference_abi_stages_match_oracle(dataset, tmp_path):
+    """InitGpu/SetOptionGpu/SetQueryGpu/SetDbGpu/SearchNextGpu/CalculateScoreGpu in
+    the order the reference aligner.cpp drives them, then TraceBackGpu, compared
+    with the oracle's per-candidate (start, score, end) and traceback dumps."""
+    d = dataset("syn_small")
+    prefix = str(tmp_path / "dump")
+    cases.run_aln(cases.ORACLE, d, ["-y", "1"], {"GHOSTM_ORACLE_DUMP": prefix}, str(tmp_path / "o"))
+    cand = np.fromfile(prefix + ".cand", dtype="<u4").reshape(-1, 4)
+    tb = np.fromfile(prefix + ".tb", dtype="<u4").reshape(-1, 5)
+
+    nq, L, qseq, dbseq, seed, kc, pos = _load_chunk(d)
+    lib = native.load()
+    m = _blosum62()
+    max_list = 1 << 27
+    assert lib.InitGpu() == 0
+    assert lib.SetOptionGpu(max_list, m.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), 0) == 0, native.last_error()
+    assert lib.SetQueryGpu(_p(qseq, ctypes.c_uint8), nq, L) == 0, native.last_error()
+    assert lib.SetDbGpu(_p(dbseq, ctypes.c_uint8), len(dbseq), _p(kc), len(kc), _p(pos), len(pos)) == 0
+    acl = np.zeros(nq + 1, dtype=np.uint32)
+    starts = np.zeros(len(cand) + 16, dtype=np.uint32)
+    qc = lib.SearchNextGpu(L, nq, seed, 2, 2, 4, max_list, 0, _p(acl), _p(starts))
+    assert qc == nq, native.last_error()
+    n = int(acl[qc])
+    assert n == len(cand)
+    qid = np.repeat(np.arange(nq, dtype=np.uint32), np.diff(acl[: qc + 1]))
+    assert np.array_equal(qid, cand[:, 0])
+    assert np.array_equal(starts[:n], cand[:, 1])
+    scores = np.zeros(n, dtype=np.uint32)
+    ends = np.zeros(n, dtype=np.uint32)
+    base = L + 2 * 2 + 2 * 16
+    lib.CalculateScoreGpu(len(dbseq), L, n, _p(scores), _p(ends), base, 2, -11, -1)
+    assert np.array_equal(scores, cand[:, 2])
+    assert np.array_equal(ends, cand[:, 3])
+    # traceback of exactly the oracle's hits
+    k = len(tb)
+    out_s, out_l, out_m = (np.zeros(k, dtype=np.uint32) for _ in range(3))
+    out_id = np.zeros(k, dtype=np.float32)
+    tqid = np.ascontiguousarray(tb[:, 0])
+    tend = np.ascontiguousarray(tb[:, 1])
+    rc = lib.TraceBackGpu(k, _p(tqid), _p(tend), L, L + 2 * 2 * 2 * 16, -11, -1, _p(out_s), _p(out_l),
+                          _p(out_m), out_id.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+    assert rc == 0, native.last_error()
+    assert np.array_equal(out_s, tb[:, 2])
+    assert np.array_equal(out_l, tb[:, 3])
+    assert np.array_equal(out_m, tb[:, 4])
+    counts = np.zeros(nq, dtype=np.uint32)
+    assert lib.CountCandidatesGpu(L, nq, seed, 2, 2, 4, _p(counts)) == 0
+    assert np.array_equal(counts, np.diff(acl[: qc + 1]))
+    assert lib.FreeGpu() == 0
+
+
+def test_reference_gpu_batching_rule(dataset):
+    """SearchNextGpu batches with the reference GPU rule (aligner_gpu.cu:911-920):
+    queries are added while the running total stays below max_number_alignments."""
+    d = dataset("syn_small")
+    nq, L, qseq, dbseq, seed, kc, pos = _load_chunk(d)
+    lib = native.load()
+    m = _blosum62()
+    assert lib.SetOptionGpu(1 << 27, m.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), 0) == 0
+    assert lib.SetQueryGpu(_p(qseq, ctypes.c_uint8), nq, L) == 0
+    assert lib.SetDbGpu(_p(dbseq, ctypes.c_uint8), len(dbseq), _p(kc), len(kc), _p(pos), len(pos)) == 0
+    counts = np.zeros(nq, dtype=np.uint32)
+    assert lib.CountCandidatesGpu(L, nq, seed, 2, 2, 4, _p(counts)) == 0
+    cap = 40
+    start, seen = 0, 0
+    acl = np.zeros(nq + 1, dtype=np.uint32)
+    starts = np.zeros(int(counts.sum()) + 16, dtype=np.uint32)
+    while True:
+        qc = lib.SearchNextGpu(L, nq, seed, 2, 2, 4, cap, start, _p(acl), _p(starts))
+        if qc == 0:
+            break
+        assert acl[qc] < cap
+        assert np.array_equal(np.diff(acl[: qc + 1]), counts[start:start + qc])
+        if start + qc < nq:
+            assert acl[qc] + counts[start + qc] >= cap
+        seen += qc
+        start += qc
+    assert seen == start
+    lib.FreeGpu()
