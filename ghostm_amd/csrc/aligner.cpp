@@ -4,16 +4,15 @@
 #include <getopt.h>
 
 #include <algorithm>
-#include <atomic>
-#include <exception>
+#include <charconv>
 #include <climits>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <fstream>
 #include <iostream>
 #include <stdexcept>
-#include <thread>
 
 #include "common.h"
 
@@ -56,6 +55,62 @@ void ParallelFor(size_t n, unsigned threads,
     if (ep) std::rethrow_exception(ep);
 }
 
+// ------------------------------------------------------------------ TaskQueue
+TaskQueue::TaskQueue() : worker_([this] { Loop(); }) {}
+
+TaskQueue::~TaskQueue() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  worker_.join();
+}
+
+void TaskQueue::Submit(std::function<void()> fn) {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    tasks_.push_back(std::move(fn));
+  }
+  cv_.notify_one();
+}
+
+void TaskQueue::Drain() {
+  std::unique_lock<std::mutex> lk(mu_);
+  idle_.wait(lk, [this] { return tasks_.empty() && !busy_; });
+  if (error_) {
+    std::exception_ptr e = error_;
+    error_ = nullptr;
+    std::rethrow_exception(e);
+  }
+}
+
+void TaskQueue::Loop() {
+  for (;;) {
+    std::function<void()> fn;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [this] { return stop_ || !tasks_.empty(); });
+      if (tasks_.empty()) return;
+      fn = std::move(tasks_.front());
+      tasks_.pop_front();
+      busy_ = true;
+    }
+    try {
+      fn();
+    } catch (...) {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (!error_) error_ = std::current_exception();
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      busy_ = false;
+    }
+    idle_.notify_all();
+  }
+}
+
+// ------------------------------------------------------------------ options
 AlignerOptions ParseAlignerOptions(int argc, char **argv) {
   AlignerOptions o;
   std::string matrix_file = "BLOSUM62";
@@ -142,6 +197,10 @@ Session::Session(const AlignerOptions &opt) : opt_(opt) {
     for (uint32_t i = n; i-- > 0;) {
       q.group_end[i] = (i + 1 < n && q.chunk.names[i + 1] == q.chunk.names[i]) ? q.group_end[i + 1] : i + 1;
     }
+    for (uint32_t i = 0; i < n; i = q.group_end[i]) {
+      q.group_first.push_back(i);
+      q.group_last.push_back(q.group_end[i] - 1);
+    }
     q.qlen.assign(n, 1);
     for (uint32_t i = 0; i < n; ++i) {
       const uint8_t *s = &q.chunk.seq[(size_t)i * L];
@@ -150,15 +209,19 @@ Session::Session(const AlignerOptions &opt) : opt_(opt) {
       q.qlen[i] = e + 1;
     }
     q.dev = dev.UploadQuery(q.chunk.seq.data(), n, L);
+    dev.SetQueryGroups(q.dev, q.group_first.data(), q.group_last.data(), (uint32_t)q.group_first.size());
   }
   for (DbData &d : dbs_) {
     const DbChunk &c = d.chunk;
     d.dev = dev.UploadDb(c.seq.data(), c.len, c.keys_count.data(), c.kcl, c.positions.data(), c.npos);
+    if (c.nseq) dev.SetDbSubjects(d.dev, c.starts.data(), c.nseq);
   }
   dev.Synchronize();
+  formatter_.reset(new TaskQueue());
 }
 
 Session::~Session() {
+  formatter_.reset();
   DeviceModule &dev = DeviceModule::Get();
   for (QueryData &q : queries_) dev.Free(q.dev);
   for (DbData &d : dbs_) dev.Free(d.dev);
@@ -216,25 +279,24 @@ struct ScoreDesc {
 // reference Merge (aligner.cpp:687-769): per name group, the batch's candidates
 // of each query then its kept results, std::sort by score (unstable), first hit
 // per subject traced back, stop at -b. Groups are independent -> host threads.
-void Session::MergeBatch(QueryData &q, DbData &d, uint32_t bq0, uint32_t bq1,
-                         uint64_t cand_begin, const uint32_t *score, const uint32_t *end,
-                         const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets,
-                         Results *results) {
-  const uint32_t n = q.chunk.nseq;
-  std::vector<uint32_t> group_starts;
-  for (uint32_t i = 0; i < n; i = q.group_end[i]) group_starts.push_back(i);
+// Used when a chunk needs several batches or several DB chunks.
+void Session::HostMergeBatch(QueryData &q, DbData &d, uint32_t bq0, uint32_t bq1,
+                             uint64_t cand_begin, const uint32_t *score, const uint32_t *end,
+                             const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets,
+                             Results *results) {
+  const uint32_t ng = (uint32_t)q.group_first.size();
   const uint64_t epoch = ++merge_epoch_;
   const uint32_t nsubj = d.chunk.nseq;
   struct Pending {
     uint32_t id, pos;
   };
   std::vector<std::vector<Pending>> pending(threads_);
-  ParallelFor(group_starts.size(), threads_, [&](size_t gb, size_t ge, unsigned t) {
+  ParallelFor(ng, threads_, [&](size_t gb, size_t ge, unsigned t) {
     std::vector<uint64_t> owner(nsubj, ~0ull);
     std::vector<MergeItem> l;
     std::vector<HitRecord> old;
     for (size_t g = gb; g < ge; ++g) {
-      const uint32_t gs = group_starts[g], gend = q.group_end[gs], id = gend - 1;
+      const uint32_t gs = q.group_first[g], gend = q.group_last[g] + 1, id = gend - 1;
       l.clear();
       old.clear();
       for (uint32_t i = gs; i < gend; ++i) {
@@ -304,7 +366,58 @@ void Session::MergeBatch(QueryData &q, DbData &d, uint32_t bq0, uint32_t bq1,
   }
 }
 
-void Session::RunQueryChunk(QueryData &q, Results *results) {
+// Device path: the chunk's groups are cut into segments of ~kSegmentCands
+// candidates (at group boundaries, so every group's candidates stay together as
+// in the single reference batch); per segment K2 -> K4 -> K3 run on the GPU and
+// the segment's text is formatted by the background worker meanwhile.
+void Session::DeviceMergePath(QueryData &q, DbData &d, const std::vector<uint32_t> &counts,
+                              const std::vector<uint64_t> &offsets, uint64_t total) {
+  DeviceModule &dev = DeviceModule::Get();
+  GapConfig gap;
+  gap.extend = opt_.extend;
+  gap.log_region = opt_.log_region;
+  gap.open = opt_.open_gap;
+  gap.ext = opt_.extend_gap;
+  const uint32_t base = q.chunk.L + 2 * opt_.extend + 2 * (1u << opt_.log_region);
+  const uint32_t tb_base = q.chunk.L + 2 * opt_.extend * 2 * (1u << opt_.log_region);
+  const uint32_t cap = std::max<uint32_t>(opt_.best, 1);
+  const uint64_t kSegmentCands = 8ull << 20;
+  const uint32_t ng = (uint32_t)q.group_first.size();
+  auto group_begin = [&](uint32_t g) { return offsets[q.group_first[g]]; };
+  uint32_t g0 = 0;
+  while (g0 < ng) {
+    uint32_t g1 = g0 + 1;
+    while (g1 < ng && group_begin(g1) - group_begin(g0) < kSegmentCands) ++g1;
+    const uint64_t c0 = group_begin(g0);
+    const uint64_t c1 = g1 < ng ? group_begin(g1) : total;
+    if (c1 > c0) {
+      dev.Score(q.dev, d.dev, c0, c1 - c0, q.group_first[g0], q.group_last[g1 - 1] + 1, counts, offsets,
+                base, gap, nullptr, nullptr);
+    }
+    auto sel_counts = std::make_shared<std::vector<uint32_t>>();
+    auto sel_hits = std::make_shared<std::vector<SelectedHit>>();
+    const double t0 = NowSeconds();
+    if (c1 > c0) {
+      dev.MergeSelect(q.dev, d.dev, g0, g1, c0, c1 - c0, opt_.best, tb_base, opt_.open_gap,
+                      opt_.extend_gap, sel_counts.get(), sel_hits.get());
+    } else {
+      sel_counts->assign(g1 - g0, 0);
+    }
+    stats_.seconds_merge += NowSeconds() - t0;
+    for (uint32_t c : *sel_counts) stats_.tracebacks += c;
+    Part *part = NewPart();
+    const QueryData *qp = &q;
+    formatter_->Submit([this, qp, g0, sel_counts, sel_hits, cap, part] {
+      const double t = NowSeconds();
+      FormatSelected(*qp, g0, *sel_counts, *sel_hits, cap, part);
+      stats_.seconds_output += NowSeconds() - t;
+    });
+    g0 = g1;
+  }
+  stats_.batches += 1;
+}
+
+void Session::RunQueryChunk(QueryData &q) {
   DeviceModule &dev = DeviceModule::Get();
   SeedConfig sc;
   sc.threshold = opt_.threshold;
@@ -319,11 +432,18 @@ void Session::RunQueryChunk(QueryData &q, Results *results) {
   std::vector<uint32_t> counts;
   std::vector<uint64_t> offsets;
   std::vector<uint32_t> score, end;
+  std::unique_ptr<Results> results;
   for (DbData &d : dbs_) {
     sc.seed_mask = d.chunk.seed;
     const uint64_t total = dev.Seed(q.dev, d.dev, sc, &counts, &offsets);
     stats_.candidates += total;
     const std::vector<Batch> batches = CpuBatches(counts, opt_.max_list_length);
+    if (dbs_.size() == 1 && batches.size() == 1 && batches[0].q0 == 0 &&
+        batches[0].q1 == q.chunk.nseq && d.chunk.nseq > 0) {
+      DeviceMergePath(q, d, counts, offsets, total);
+      return;
+    }
+    if (!results) results.reset(new Results(q.chunk.nseq));
     for (const Batch &b : batches) {
       const uint64_t c0 = offsets[b.q0];
       const uint64_t c1 = b.q1 < counts.size() ? offsets[b.q1] : total;
@@ -332,11 +452,16 @@ void Session::RunQueryChunk(QueryData &q, Results *results) {
       end.resize(nc);
       dev.Score(q.dev, d.dev, c0, nc, b.q0, b.q1, counts, offsets, base, gap, score.data(), end.data());
       const double t0 = NowSeconds();
-      MergeBatch(q, d, b.q0, b.q1, c0, score.data(), end.data(), counts, offsets, results);
+      HostMergeBatch(q, d, b.q0, b.q1, c0, score.data(), end.data(), counts, offsets, results.get());
       stats_.seconds_merge += NowSeconds() - t0;
       stats_.batches += 1;
     }
   }
+  if (!results) results.reset(new Results(q.chunk.nseq));
+  formatter_->Drain();
+  const double t1 = NowSeconds();
+  FormatResults(q, *results, NewPart());
+  stats_.seconds_output += NowSeconds() - t1;
 }
 
 // ------------------------------------------------------------------ output
@@ -347,92 +472,132 @@ inline void AppendU32(std::string *s, uint32_t v) {
   do { buf[n++] = (char)('0' + v % 10); v /= 10; } while (v);
   while (n) s->push_back(buf[--n]);
 }
+// ostream << float == printf("%g") == to_chars(general, 6) (checked on 6e8 bit
+// patterns incl. NaN/inf/denormals), and to_chars is ~5x faster than snprintf.
 inline void AppendFloat(std::string *s, float f) {
   char buf[48];
-  const int n = snprintf(buf, sizeof(buf), "%g", (double)f);
-  s->append(buf, n);
+  const auto r = std::to_chars(buf, buf + sizeof(buf), f, std::chars_format::general, 6);
+  s->append(buf, r.ptr - buf);
 }
+
+// One output line, WriteOutput / V1 / V2 (aligner.cpp:951-1012).
+struct LineWriter {
+  int style;
+  EvalueCalculator ev;
+  void Write(std::string *s, const std::string &qname, const std::string &sname, uint32_t score,
+             uint32_t start, uint32_t end, uint32_t len, uint32_t match, float seq_id,
+             uint64_t space) const {
+    s->append(qname);
+    s->push_back('\t');
+    s->append(sname);
+    s->push_back('\t');
+    if (style == 1) {
+      AppendU32(s, score); s->push_back('\t');
+      AppendU32(s, start + 1); s->push_back('\t');
+      AppendU32(s, end + 1);
+    } else if (style == 2) {
+      AppendU32(s, score); s->push_back('\t');
+      AppendU32(s, start + 1); s->push_back('\t');
+      AppendU32(s, end + 1); s->push_back('\t');
+      AppendFloat(s, seq_id); s->push_back('\t');
+      AppendU32(s, len); s->push_back('\t');
+      AppendU32(s, match);
+    } else {
+      AppendFloat(s, seq_id * 100); s->push_back('\t');
+      AppendU32(s, len); s->push_back('\t');
+      AppendU32(s, match); s->push_back('\t');
+      AppendU32(s, start + 1); s->push_back('\t');
+      AppendU32(s, end + 1); s->push_back('\t');
+      AppendFloat(s, ev.Evalue((int)score, space)); s->push_back('\t');
+      AppendFloat(s, ev.Bits((int)score)); s->push_back('\t');
+    }
+    s->push_back('\n');
+  }
+};
 }  // namespace
 
-// WriteOutput / V1 / V2 (aligner.cpp:951-1012): ostream << float prints "%g".
-void Session::FormatChunk(const QueryData &q, const Results &results, std::string *text,
-                          std::vector<GhostmHit> *hits) {
+Session::Part *Session::NewPart() {
+  parts_.emplace_back();
+  return &parts_.back();
+}
+
+void Session::FormatResults(const QueryData &q, const Results &results, Part *out) {
   const uint32_t n = q.chunk.nseq;
-  std::vector<std::string> parts(threads_);
-  std::vector<std::vector<GhostmHit>> hparts(threads_);
-  const EvalueCalculator ev(opt_.karlin);
-  const int style = opt_.output_style;
+  std::vector<Part> local(threads_);
+  const LineWriter w{opt_.output_style, EvalueCalculator(opt_.karlin)};
   ParallelFor(n, threads_, [&](size_t b, size_t e, unsigned t) {
-    std::string &s = parts[t];
-    std::vector<GhostmHit> &hv = hparts[t];
+    Part &p = local[t];
     for (size_t i = b; i < e; ++i) {
-      const std::string &name = q.chunk.names[i];
       const uint64_t space = (uint64_t)q.qlen[i] * (uint64_t)db_sum_u32_;
       for (const HitRecord &h : results[i]) {
         const DbData &d = dbs_[h.db_chunk];
-        const std::string &sname = d.chunk.names[h.subject];
-        s.append(name);
-        s.push_back('\t');
-        s.append(sname);
-        s.push_back('\t');
-        if (style == 1) {
-          AppendU32(&s, h.score); s.push_back('\t');
-          AppendU32(&s, h.start + 1); s.push_back('\t');
-          AppendU32(&s, h.end + 1);
-        } else if (style == 2) {
-          AppendU32(&s, h.score); s.push_back('\t');
-          AppendU32(&s, h.start + 1); s.push_back('\t');
-          AppendU32(&s, h.end + 1); s.push_back('\t');
-          AppendFloat(&s, h.seq_id); s.push_back('\t');
-          AppendU32(&s, h.aln_len); s.push_back('\t');
-          AppendU32(&s, h.aln_match);
-        } else {
-          AppendFloat(&s, h.seq_id * 100); s.push_back('\t');
-          AppendU32(&s, h.aln_len); s.push_back('\t');
-          AppendU32(&s, h.aln_match); s.push_back('\t');
-          AppendU32(&s, h.start + 1); s.push_back('\t');
-          AppendU32(&s, h.end + 1); s.push_back('\t');
-          AppendFloat(&s, ev.Evalue((int)h.score, space)); s.push_back('\t');
-          AppendFloat(&s, ev.Bits((int)h.score)); s.push_back('\t');
-        }
-        s.push_back('\n');
-        GhostmHit g;
-        g.query_id = q.global_base + (uint32_t)i;
-        g.db_id = d.global_base + h.subject;
-        g.score = h.score;
-        g.db_start = h.start;
-        g.db_end = h.end;
-        g.aln_len = h.aln_len;
-        g.aln_match = h.aln_match;
-        g.seq_id = h.seq_id;
-        hv.push_back(g);
+        w.Write(&p.text, q.chunk.names[i], d.chunk.names[h.subject], h.score, h.start, h.end, h.aln_len,
+                h.aln_match, h.seq_id, space);
+        p.hits.push_back(GhostmHit{q.global_base + (uint32_t)i, d.global_base + h.subject, h.score, h.start,
+                                   h.end, h.aln_len, h.aln_match, h.seq_id});
       }
     }
   });
-  size_t add = 0;
-  for (auto &p : parts) add += p.size();
-  text->reserve(text->size() + add);
-  for (auto &p : parts) text->append(p);
-  for (auto &h : hparts) hits->insert(hits->end(), h.begin(), h.end());
+  for (Part &p : local) {
+    out->text.append(p.text);
+    out->hits.insert(out->hits.end(), p.hits.begin(), p.hits.end());
+  }
+}
+
+// Same text from the device-selected hits: a name group's lines are printed
+// under its last query (the reference's result_list[last]).
+void Session::FormatSelected(const QueryData &q, uint32_t g0, const std::vector<uint32_t> &counts,
+                             const std::vector<SelectedHit> &hits, uint32_t cap, Part *out) {
+  const uint32_t ng = (uint32_t)counts.size();
+  const unsigned workers = std::max(1u, threads_ > 1 ? threads_ - 1 : 1u);
+  std::vector<Part> local(workers);
+  const LineWriter w{opt_.output_style, EvalueCalculator(opt_.karlin)};
+  const DbData &d = dbs_[0];
+  ParallelFor(ng, workers, [&](size_t b, size_t e, unsigned t) {
+    Part &p = local[t];
+    p.text.reserve((e - b) * cap * 64);
+    for (size_t g = b; g < e; ++g) {
+      const uint32_t i = q.group_last[g0 + g];
+      const std::string &name = q.chunk.names[i];
+      const uint64_t space = (uint64_t)q.qlen[i] * (uint64_t)db_sum_u32_;
+      for (uint32_t k = 0; k < counts[g]; ++k) {
+        const SelectedHit &h = hits[(size_t)g * cap + k];
+        const uint32_t len = h.ml >> 8, match = h.ml & 0xFFu;
+        const float seq_id = (float)match / (float)len;  // aligner.cpp:945
+        w.Write(&p.text, name, d.chunk.names[h.sid], h.score, h.start, h.end, len, match, seq_id, space);
+        p.hits.push_back(GhostmHit{q.global_base + i, d.global_base + h.sid, h.score, h.start, h.end, len,
+                                   match, seq_id});
+      }
+    }
+  });
+  size_t bytes = 0, nh = 0;
+  for (Part &p : local) { bytes += p.text.size(); nh += p.hits.size(); }
+  out->text.reserve(bytes);
+  out->hits.reserve(nh);
+  for (Part &p : local) {
+    out->text.append(p.text);
+    out->hits.insert(out->hits.end(), p.hits.begin(), p.hits.end());
+  }
 }
 
 void Session::Run() {
   DeviceModule &dev = DeviceModule::Get();
+  formatter_->Drain();
   dev.ResetTimes();
   stats_ = GhostmStats{};
   merge_epoch_ = 0;
-  output_.clear();
+  parts_.clear();
+  joined_.clear();
+  joined_valid_ = false;
   hits_.clear();
+  hits_valid_ = false;
   const double t0 = NowSeconds();
   for (QueryData &q : queries_) {
-    Results results(q.chunk.nseq);
-    RunQueryChunk(q, &results);
-    const double t1 = NowSeconds();
-    FormatChunk(q, results, &output_, &hits_);
-    stats_.seconds_output += NowSeconds() - t1;
+    RunQueryChunk(q);
     stats_.queries += q.chunk.nseq;
     for (uint32_t v : q.qlen) stats_.query_residues += v;
   }
+  formatter_->Drain();
   stats_.seconds_total = NowSeconds() - t0;
   const DeviceTimes &dt = dev.times();
   stats_.seconds_seed = dt.seed;
@@ -440,12 +605,35 @@ void Session::Run() {
   stats_.seconds_traceback = dt.traceback;
   stats_.score_launches = dt.score_launches;
   stats_.seed_bytes = dt.seed_bytes;
-  stats_.hits = hits_.size();
+  stats_.score_cells = dt.score_cells;
+  stats_.traceback_cells = dt.traceback_cells;
+  for (const Part &p : parts_) stats_.hits += p.hits.size();
 }
 
-void Session::WriteOutputFile() const {
+const std::string &Session::Output() {
+  if (!joined_valid_) {
+    size_t n = 0;
+    for (const Part &p : parts_) n += p.text.size();
+    joined_.clear();
+    joined_.reserve(n);
+    for (const Part &p : parts_) joined_.append(p.text);
+    joined_valid_ = true;
+  }
+  return joined_;
+}
+
+const std::vector<GhostmHit> &Session::Hits() {
+  if (!hits_valid_) {
+    hits_.clear();
+    for (const Part &p : parts_) hits_.insert(hits_.end(), p.hits.begin(), p.hits.end());
+    hits_valid_ = true;
+  }
+  return hits_;
+}
+
+void Session::WriteOutputFile() {
   std::ofstream out(opt_.output_file.c_str(), std::ios::binary);
-  out.write(output_.data(), (std::streamsize)output_.size());
+  for (const Part &p : parts_) out.write(p.text.data(), (std::streamsize)p.text.size());
 }
 
 }  // namespace ghostm

@@ -2,14 +2,21 @@
 // aligner.cpp:65-1012) re-built around the gfx950 device module.
 //
 // Same options, same chunk loops, same batch cuts, same Merge order (libstdc++
-// std::sort), same tie rules and the same text output as the reference CPU path;
-// the seed search, score DP and traceback run on the GPU, the merge selection and
-// the output formatting run on host threads.
+// std::sort), same tie rules and the same text output as the reference CPU path.
+// Seed search, score DP, merge selection and traceback run on the GPU when a query
+// chunk is one batch against one DB chunk (the common case, and the benchmark);
+// otherwise the merge runs on host threads with the reference's exact semantics.
+// Output text is produced by a background formatter while the GPU works on the
+// next segment.
 #pragma once
+#include <condition_variable>
 #include <cstdint>
+#include <deque>
 #include <functional>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/ghostm_hip.h"
@@ -58,15 +65,38 @@ struct HitRecord {
   float seq_id = 0.f;
 };
 
+// Number of host worker threads (GHOSTM_THREADS, default min(16, hardware)).
+unsigned HostThreads();
+
+// Parallel for over [0, n) in contiguous blocks.
+void ParallelFor(size_t n, unsigned threads, const std::function<void(size_t, size_t, unsigned)> &fn);
+
+// One background thread running submitted tasks in order.
+class TaskQueue {
+ public:
+  TaskQueue();
+  ~TaskQueue();
+  void Submit(std::function<void()> fn);
+  void Drain();  // waits for every submitted task; rethrows the first error
+ private:
+  void Loop();
+  std::mutex mu_;
+  std::condition_variable cv_, idle_;
+  std::deque<std::function<void()>> tasks_;
+  bool stop_ = false, busy_ = false;
+  std::exception_ptr error_;
+  std::thread worker_;
+};
+
 class Session {
  public:
   explicit Session(const AlignerOptions &opt);
   ~Session();
 
-  void Run();                       // whole search; replaces previous results
-  const std::string &Output() const { return output_; }
-  void WriteOutputFile() const;
-  const std::vector<GhostmHit> &Hits() const { return hits_; }
+  void Run();                          // whole search; replaces previous results
+  const std::string &Output();         // text of the last run (joined on first use)
+  void WriteOutputFile();
+  const std::vector<GhostmHit> &Hits();
   const GhostmStats &Stats() const { return stats_; }
 
  private:
@@ -74,6 +104,7 @@ class Session {
     QueryChunk chunk;
     DevQuery *dev = nullptr;
     std::vector<uint32_t> group_end;   // per query: one past the last query of its name group
+    std::vector<uint32_t> group_first, group_last;  // name groups in order
     std::vector<uint32_t> qlen;        // WriteOutput's query length (last non-X + 1)
     uint32_t global_base = 0;          // index of the chunk's first query over all chunks
   };
@@ -82,30 +113,37 @@ class Session {
     DevDb *dev = nullptr;
     uint32_t global_base = 0;
   };
-
+  // Output of one segment, in output order.
+  struct Part {
+    std::string text;
+    std::vector<GhostmHit> hits;
+  };
   using Results = std::vector<std::vector<HitRecord>>;
-  void RunQueryChunk(QueryData &q, Results *results);
-  void MergeBatch(QueryData &q, DbData &d, uint32_t bq0, uint32_t bq1, uint64_t cand_begin,
-                  const uint32_t *score, const uint32_t *end, const std::vector<uint32_t> &counts,
-                  const std::vector<uint64_t> &offsets, Results *results);
-  void FormatChunk(const QueryData &q, const Results &results, std::string *text,
-                   std::vector<GhostmHit> *hits);
+
+  void RunQueryChunk(QueryData &q);
+  void DeviceMergePath(QueryData &q, DbData &d, const std::vector<uint32_t> &counts,
+                       const std::vector<uint64_t> &offsets, uint64_t total);
+  void HostMergeBatch(QueryData &q, DbData &d, uint32_t bq0, uint32_t bq1, uint64_t cand_begin,
+                      const uint32_t *score, const uint32_t *end, const std::vector<uint32_t> &counts,
+                      const std::vector<uint64_t> &offsets, Results *results);
+  void FormatResults(const QueryData &q, const Results &results, Part *out);
+  void FormatSelected(const QueryData &q, uint32_t g0, const std::vector<uint32_t> &counts,
+                      const std::vector<SelectedHit> &hits, uint32_t cap, Part *out);
+  Part *NewPart();
 
   AlignerOptions opt_;
   std::vector<QueryData> queries_;
   std::vector<DbData> dbs_;
   uint32_t db_sum_u32_ = 0;           // DBReader::GetSumDbLength() truncates to u32
   uint64_t merge_epoch_ = 0;
-  std::string output_;
+  std::deque<Part> parts_;
+  std::string joined_;
+  bool joined_valid_ = false;
   std::vector<GhostmHit> hits_;
+  bool hits_valid_ = false;
   GhostmStats stats_{};
   unsigned threads_ = 1;
+  std::unique_ptr<TaskQueue> formatter_;
 };
-
-// Number of host worker threads (GHOSTM_THREADS, default min(16, hardware)).
-unsigned HostThreads();
-
-// Parallel for over [0, n) in contiguous blocks.
-void ParallelFor(size_t n, unsigned threads, const std::function<void(size_t, size_t, unsigned)> &fn);
 
 }  // namespace ghostm

@@ -34,10 +34,17 @@ struct GapConfig {
 struct DevQuery;
 struct DevDb;
 
+// One hit chosen by the device merge (K4), after its traceback (K3):
+// subject-relative coordinates, ml = (aln_len << 8) | matches.
+struct SelectedHit {
+  uint32_t sid, score, start, end, ml;
+};
+
 struct DeviceTimes {
-  double seed = 0, score = 0, traceback = 0;  // seconds of device time (HIP events)
+  double seed = 0, score = 0, traceback = 0, merge = 0;  // seconds of device time (HIP events)
   uint64_t seed_bytes = 0;
   uint64_t score_launches = 0;
+  uint64_t score_cells = 0, traceback_cells = 0;
 };
 
 class DeviceModule {
@@ -53,6 +60,10 @@ class DeviceModule {
   DevQuery *UploadQuery(const uint8_t *seq, uint32_t nseq, uint32_t L);
   DevDb *UploadDb(const uint8_t *seq, uint32_t len, const uint32_t *keys_count, uint32_t kcl,
                   const uint32_t *positions, uint32_t npos);
+  // Name groups of a query chunk (consecutive equal names), for the device merge.
+  void SetQueryGroups(DevQuery *q, const uint32_t *first, const uint32_t *last, uint32_t ng);
+  // Subject start offsets (.pos) of a DB chunk, for the device merge.
+  void SetDbSubjects(DevDb *d, const uint32_t *starts, uint32_t nsubj);
   void Free(DevQuery *q);
   void Free(DevDb *d);
 
@@ -71,6 +82,15 @@ class DeviceModule {
              uint32_t q_end, const std::vector<uint32_t> &counts,
              const std::vector<uint64_t> &offsets, uint32_t base_search_length,
              const GapConfig &gap, uint32_t *score, uint32_t *end);
+
+  // K4 + K3 for a batch that covers every group of the chunk and starts from
+  // empty result lists (first batch, first DB chunk): the reference Merge
+  // selection on the device, then the traceback of every selected hit. Uses the
+  // scores/ends left on the device by the preceding Score() over the same range.
+  // counts[g] hits per group; hits[g*cap + k], cap = max(best, 1).
+  void MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, uint64_t cand_begin, uint64_t n, uint32_t best,
+                   uint32_t tb_base, int open, int ext, std::vector<uint32_t> *counts,
+                   std::vector<SelectedHit> *hits);
 
   // K3 on n hits (query id, absolute db end).
   void TraceBack(DevQuery *q, DevDb *d, uint32_t n, const uint32_t *qid, const uint32_t *db_end,

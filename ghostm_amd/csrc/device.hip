@@ -77,11 +77,15 @@ thread_local std::string g_last_error;
 struct DevQuery {
   DevBuf seq;
   uint32_t nseq = 0, L = 0;
+  DevBuf group_first, group_last;  // name groups (device merge)
+  uint32_t ngroups = 0;
 };
 
 struct DevDb {
   DevBuf seq, kc, pos;
   uint32_t len = 0, kcl = 0, npos = 0;
+  DevBuf subj;                     // subject starts (device merge)
+  uint32_t nsubj = 0;
 };
 
 struct DeviceModule::Impl {
@@ -95,7 +99,10 @@ struct DeviceModule::Impl {
   DevBuf tasks, score_out, end_out;
   // K3 work
   DevBuf tb_qid, tb_end, tb_start, tb_ml;
+  // K4 work
+  DevBuf keys, sel_count, sel_cand, sel_sid, slot_hits;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  DevBuf counters;  // u64 [0] score cells, [1] traceback cells
   bool matrix_set = false;
 };
 
@@ -191,6 +198,8 @@ DevDb *DeviceModule::UploadDb(const uint8_t *seq, uint32_t len, const uint32_t *
 void DeviceModule::Free(DevQuery *q) {
   if (!q) return;
   q->seq.Release();
+  q->group_first.Release();
+  q->group_last.Release();
   delete q;
 }
 
@@ -199,7 +208,25 @@ void DeviceModule::Free(DevDb *d) {
   d->seq.Release();
   d->kc.Release();
   d->pos.Release();
+  d->subj.Release();
   delete d;
+}
+
+void DeviceModule::SetQueryGroups(DevQuery *q, const uint32_t *first, const uint32_t *last,
+                                  uint32_t ng) {
+  q->ngroups = ng;
+  q->group_first.Reserve((size_t)ng * 4);
+  q->group_last.Reserve((size_t)ng * 4);
+  if (ng) {
+    HIP_CHECK(hipMemcpy(q->group_first.p, first, (size_t)ng * 4, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(q->group_last.p, last, (size_t)ng * 4, hipMemcpyHostToDevice));
+  }
+}
+
+void DeviceModule::SetDbSubjects(DevDb *d, const uint32_t *starts, uint32_t nsubj) {
+  d->nsubj = nsubj;
+  d->subj.Reserve((size_t)nsubj * 4);
+  if (nsubj) HIP_CHECK(hipMemcpy(d->subj.p, starts, (size_t)nsubj * 4, hipMemcpyHostToDevice));
 }
 
 void DeviceModule::Synchronize() {
@@ -408,6 +435,9 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
   a.score_out = I.score_out.as<uint32_t>();
   a.end_out = I.end_out.as<uint32_t>();
   a.out_base = cand_begin;
+  I.counters.Reserve(16);
+  HIP_CHECK(hipMemsetAsync(I.counters.p, 0, 16, S(stream_)));
+  a.cells = I.counters.as<unsigned long long>();
   const size_t lds = (size_t)kern::kScoreQmax * kern::kProfRows * (lay.Lpad + 4) * 4;
   HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
   const dim3 grid((uint32_t)tasks.size()), block(kern::kScoreBlock);
@@ -418,11 +448,111 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
   }
   HIP_CHECK(hipGetLastError());
   HIP_CHECK(hipEventRecord(I.ev1, S(stream_)));
-  HIP_CHECK(hipMemcpyAsync(score, I.score_out.p, n * 4, hipMemcpyDeviceToHost, S(stream_)));
-  HIP_CHECK(hipMemcpyAsync(end, I.end_out.p, n * 4, hipMemcpyDeviceToHost, S(stream_)));
+  if (score) HIP_CHECK(hipMemcpyAsync(score, I.score_out.p, n * 4, hipMemcpyDeviceToHost, S(stream_)));
+  if (end) HIP_CHECK(hipMemcpyAsync(end, I.end_out.p, n * 4, hipMemcpyDeviceToHost, S(stream_)));
+  unsigned long long cells = 0;
+  HIP_CHECK(hipMemcpyAsync(&cells, I.counters.p, 8, hipMemcpyDeviceToHost, S(stream_)));
   HIP_CHECK(hipStreamSynchronize(S(stream_)));
   times_.score += ElapsedMs(I.ev0, I.ev1) * 1e-3;
   times_.score_launches += 1;
+  times_.score_cells += cells;
+}
+
+void DeviceModule::MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, uint64_t cand_begin, uint64_t n,
+                               uint32_t best, uint32_t tb_base, int open, int ext,
+                               std::vector<uint32_t> *counts, std::vector<SelectedHit> *hits) {
+  Impl &I = *impl_;
+  if (g1 > q->ngroups || g0 > g1) throw Error("group range outside the chunk");
+  const uint32_t ng = g1 - g0;
+  const uint32_t cap = std::max<uint32_t>(best, 1);
+  counts->assign(ng, 0);
+  hits->clear();
+  if (ng == 0) return;
+  if (d->nsubj == 0) throw Error("DB subjects not set for the device merge");
+  const size_t slots = (size_t)ng * cap;
+  I.keys.Reserve(n * 8 + 8);
+  I.sel_count.Reserve((size_t)ng * 4);
+  I.sel_cand.Reserve(slots * 4);
+  I.sel_sid.Reserve(slots * 4);
+  I.tb_qid.Reserve(slots * 4);
+  I.tb_end.Reserve(slots * 4);
+  I.tb_start.Reserve(slots * 4);
+  I.tb_ml.Reserve(slots * 4);
+  I.slot_hits.Reserve(slots * sizeof(kern::SlotHit));
+  kern::MergeArgs m{};
+  m.group_first = q->group_first.as<uint32_t>() + g0;
+  m.group_last = q->group_last.as<uint32_t>() + g0;
+  m.ng = ng;
+  m.offsets = I.offsets.as<unsigned long long>();
+  m.counts = I.counts.as<uint32_t>();
+  m.out_base = cand_begin;
+  m.score = I.score_out.as<uint32_t>();
+  m.end = I.end_out.as<uint32_t>();
+  m.cand_qid = I.cand_qid.as<uint32_t>();
+  m.subj_start = d->subj.as<uint32_t>();
+  m.nsubj = d->nsubj;
+  m.dblen = d->len;
+  m.keys = I.keys.as<unsigned long long>();
+  m.best = best;
+  m.cap = cap;
+  m.sel_count = I.sel_count.as<uint32_t>();
+  m.sel_cand = I.sel_cand.as<uint32_t>();
+  m.sel_sid = I.sel_sid.as<uint32_t>();
+  m.tb_qid = I.tb_qid.as<uint32_t>();
+  m.tb_end = I.tb_end.as<uint32_t>();
+  HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
+  hipLaunchKernelGGL(kern::k_merge, dim3((ng + 255) / 256), dim3(256), 0, S(stream_), m);
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipEventRecord(I.ev1, S(stream_)));
+  times_.merge += ElapsedMs(I.ev0, I.ev1) * 1e-3;
+
+  // K3 over the slots (empty slots carry qid 0xFFFFFFFF and are skipped)
+  const Layout lay = ChooseLayout(q->L, tb_base);
+  kern::TbArgs a{};
+  a.qseq = q->seq.as<uint8_t>();
+  a.L = q->L;
+  a.Lpad = lay.Lpad;
+  a.G = lay.G;
+  a.gpw = lay.gpw;
+  a.db = d->seq.as<uint8_t>();
+  a.mat_tb = I.mat_tb.as<int>();
+  a.qid = I.tb_qid.as<uint32_t>();
+  a.end = I.tb_end.as<uint32_t>();
+  a.n = (uint32_t)slots;
+  a.base = tb_base;
+  a.open = open;
+  a.ext = ext;
+  a.out_start = I.tb_start.as<uint32_t>();
+  a.out_ml = I.tb_ml.as<uint32_t>();
+  I.counters.Reserve(16);
+  HIP_CHECK(hipMemsetAsync(I.counters.p, 0, 16, S(stream_)));
+  a.cells = I.counters.as<unsigned long long>() + 1;
+  const uint32_t per_block = (kern::kTbBlock / 64) * lay.gpw;
+  const dim3 grid((uint32_t)((slots + per_block - 1) / per_block)), block(kern::kTbBlock);
+  HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
+  switch (lay.S) {
+    case 32: hipLaunchKernelGGL(kern::k_traceback<32>, grid, block, 0, S(stream_), a); break;
+    case 16: hipLaunchKernelGGL(kern::k_traceback<16>, grid, block, 0, S(stream_), a); break;
+    default: hipLaunchKernelGGL(kern::k_traceback<8>, grid, block, 0, S(stream_), a); break;
+  }
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipEventRecord(I.ev1, S(stream_)));
+  hipLaunchKernelGGL(kern::k_finalize, dim3((uint32_t)((slots + 255) / 256)), dim3(256), 0, S(stream_),
+                     I.sel_count.as<uint32_t>(), I.sel_cand.as<uint32_t>(), I.sel_sid.as<uint32_t>(),
+                     I.score_out.as<uint32_t>(), I.end_out.as<uint32_t>(), I.tb_start.as<uint32_t>(),
+                     I.tb_ml.as<uint32_t>(), d->subj.as<uint32_t>(), ng, cap,
+                     I.slot_hits.as<kern::SlotHit>());
+  HIP_CHECK(hipGetLastError());
+  static_assert(sizeof(kern::SlotHit) == sizeof(SelectedHit), "record layout");
+  hits->resize(slots);
+  unsigned long long cells = 0;
+  HIP_CHECK(hipMemcpyAsync(counts->data(), I.sel_count.p, (size_t)ng * 4, hipMemcpyDeviceToHost, S(stream_)));
+  HIP_CHECK(hipMemcpyAsync(hits->data(), I.slot_hits.p, slots * sizeof(SelectedHit), hipMemcpyDeviceToHost,
+                           S(stream_)));
+  HIP_CHECK(hipMemcpyAsync(&cells, I.counters.as<unsigned long long>() + 1, 8, hipMemcpyDeviceToHost, S(stream_)));
+  HIP_CHECK(hipStreamSynchronize(S(stream_)));
+  times_.traceback += ElapsedMs(I.ev0, I.ev1) * 1e-3;
+  times_.traceback_cells += cells;
 }
 
 void DeviceModule::TraceBack(DevQuery *q, DevDb *d, uint32_t n, const uint32_t *qid,
@@ -454,6 +584,9 @@ void DeviceModule::TraceBack(DevQuery *q, DevDb *d, uint32_t n, const uint32_t *
   a.ext = ext;
   a.out_start = I.tb_start.as<uint32_t>();
   a.out_ml = I.tb_ml.as<uint32_t>();
+  I.counters.Reserve(16);
+  HIP_CHECK(hipMemsetAsync(I.counters.p, 0, 16, S(stream_)));
+  a.cells = I.counters.as<unsigned long long>() + 1;
   const uint32_t per_block = (kern::kTbBlock / 64) * lay.gpw;
   const dim3 grid((n + per_block - 1) / per_block), block(kern::kTbBlock);
   HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
@@ -467,8 +600,11 @@ void DeviceModule::TraceBack(DevQuery *q, DevDb *d, uint32_t n, const uint32_t *
   std::vector<uint32_t> ml(n);
   HIP_CHECK(hipMemcpyAsync(db_start, I.tb_start.p, (size_t)n * 4, hipMemcpyDeviceToHost, S(stream_)));
   HIP_CHECK(hipMemcpyAsync(ml.data(), I.tb_ml.p, (size_t)n * 4, hipMemcpyDeviceToHost, S(stream_)));
+  unsigned long long cells = 0;
+  HIP_CHECK(hipMemcpyAsync(&cells, I.counters.as<unsigned long long>() + 1, 8, hipMemcpyDeviceToHost, S(stream_)));
   HIP_CHECK(hipStreamSynchronize(S(stream_)));
   times_.traceback += ElapsedMs(I.ev0, I.ev1) * 1e-3;
+  times_.traceback_cells += cells;
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t len = ml[i] >> 8, match = ml[i] & 0xFFu;
     if (aln_len) aln_len[i] = len;

@@ -14,9 +14,15 @@
 // K3 k_traceback the reverse DP of TraceBack with the same lane-group layout, the
 //                (match, length) bookkeeping packed into one int per row.
 //                reference aligner.cpp:800-947.
+// K4 k_merge     one lane per name group: the reference Merge selection
+//                (aligner.cpp:697-768) — std::sort permutation reproduced by
+//                libstdcxx_sort.h, first hit per subject, stop at -b — writing
+//                the traceback requests of K3 in place.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include "libstdcxx_sort.h"
 
 namespace ghostm {
 namespace kern {
@@ -255,6 +261,12 @@ __global__ void k_compact(const uint32_t *slots, uint32_t slot_cap, const uint32
   }
 }
 
+// One atomic per wave for a work counter.
+__device__ inline void WaveAddCells(unsigned long long *counter, unsigned long long v) {
+  for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d);
+  if ((threadIdx.x & 63) == 0 && counter && v) atomicAdd(counter, v);
+}
+
 // ------------------------------------------------------------------ K2 score
 constexpr int kScoreBlock = 256;
 constexpr int kScoreQmax = 4;
@@ -282,6 +294,7 @@ struct ScoreArgs {
   uint32_t *score_out;
   uint32_t *end_out;
   unsigned long long out_base;
+  unsigned long long *cells;  // += L x non-END window columns (work counter)
 };
 
 template <int S>
@@ -324,6 +337,7 @@ __global__ __launch_bounds__(kScoreBlock) void k_score(ScoreArgs a) {
 #pragma unroll
   for (int k = 0; k < S; ++k) { H[k] = 0; E[k] = 0; }
   int best = 0, best_col = 0;
+  uint32_t ncols = 0;
   int hout = 0, fout = 0, hprev = 0;
   const int open = a.open, ext = a.ext;
   int j = -(int)i;
@@ -366,6 +380,7 @@ __global__ __launch_bounds__(kScoreBlock) void k_score(ScoreArgs a) {
         hout = H[S - 1];
         fout = F;
         if (cm >= best) { best = cm; best_col = j; }
+        ++ncols;
       }
     }
   }
@@ -379,6 +394,7 @@ __global__ __launch_bounds__(kScoreBlock) void k_score(ScoreArgs a) {
     a.score_out[cand - a.out_base] = (uint32_t)B;
     a.end_out[cand - a.out_base] = off + (uint32_t)C;
   }
+  WaveAddCells(a.cells, (valid && i == 0) ? (unsigned long long)ncols * a.L : 0ull);
 }
 
 // ------------------------------------------------------------------ K3 traceback
@@ -396,6 +412,7 @@ struct TbArgs {
   int open, ext;
   uint32_t *out_start;
   uint32_t *out_ml;           // (aln_len << 8) | matches
+  unsigned long long *cells;  // += L x processed columns (work counter)
 };
 
 template <int S>
@@ -407,7 +424,7 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback(TbArgs a) {
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t g = lane / a.G, i = lane - g * a.G;
   const uint32_t hit = (blockIdx.x * (kTbBlock / 64) + wave) * a.gpw + g;
-  const bool valid = g < a.gpw && hit < a.n;
+  const bool valid = g < a.gpw && hit < a.n && a.qid[hit] != 0xFFFFFFFFu;
   uint32_t p0 = 0, width = 0;
   // processing row U = i*S + u walks the query backwards: position L-1-(U-pad)
   uint32_t qcode[S / 4];
@@ -430,6 +447,7 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback(TbArgs a) {
   int best = 0, best_col = 0, best_ml = 0;
   int hout = 0, fout = 0, mout = 0, hprev = 0, mprev = 0;
   bool done = false;
+  uint32_t ncols = 0;
   const int open = a.open, ext = a.ext;
   int j = -(int)i;
   const uint32_t steps = a.base + a.G - 1;
@@ -470,6 +488,7 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback(TbArgs a) {
       hout = H[S - 1];
       fout = F;
       mout = M[S - 1];
+      ++ncols;
     } else {
       hout = 0; fout = 0; mout = 0;
     }
@@ -485,6 +504,96 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback(TbArgs a) {
     a.out_start[hit] = p0 - (uint32_t)C;
     a.out_ml[hit] = (uint32_t)ML;
   }
+  WaveAddCells(a.cells, (valid && i == 0) ? (unsigned long long)ncols * a.L : 0ull);
+}
+
+// ------------------------------------------------------------------ K4 merge
+struct MergeArgs {
+  const uint32_t *group_first;         // [ng] first query of the name group
+  const uint32_t *group_last;          // [ng] last query (the printed index)
+  uint32_t ng;
+  const unsigned long long *offsets;   // per query, absolute candidate index
+  const uint32_t *counts;              // per query
+  unsigned long long out_base;         // absolute index of batch-relative 0
+  const uint32_t *score;               // batch-relative
+  const uint32_t *end;                 // batch-relative, absolute DB position
+  const uint32_t *cand_qid;            // absolute
+  const uint32_t *subj_start;          // DB chunk subject starts (.pos)
+  uint32_t nsubj, dblen;
+  unsigned long long *keys;            // scratch, batch-relative
+  uint32_t best, cap;                  // -b and slots per group (max(best, 1))
+  uint32_t *sel_count;                 // [ng]
+  uint32_t *sel_cand;                  // [ng*cap] batch-relative candidate
+  uint32_t *sel_sid;                   // [ng*cap]
+  uint32_t *tb_qid;                    // [ng*cap] K3 request (0xFFFFFFFF = empty)
+  uint32_t *tb_end;                    // [ng*cap]
+};
+
+// DB::GetID (db.h:106-135), unsigned arithmetic as the reference.
+__device__ inline uint32_t SubjectOf(const uint32_t *starts, uint32_t n, uint32_t len, uint32_t p) {
+  if (starts[n - 1] <= p && p < len) return n - 1;
+  uint32_t lo = 0, hi = n - 2;
+  while (lo <= hi) {
+    const uint32_t mid = (lo + hi) / 2;
+    if (starts[mid] <= p && p < starts[mid + 1]) return mid;
+    if (starts[mid] < p) lo = mid + 1; else hi = mid - 1;
+  }
+  return 0xFFFFFFFFu;
+}
+
+struct ScoreDescending {
+  __device__ bool operator()(unsigned long long x, unsigned long long y) const {
+    return (uint32_t)(x >> 32) > (uint32_t)(y >> 32);
+  }
+};
+
+__global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= a.ng) return;
+  const uint32_t q0 = a.group_first[g], q1 = a.group_last[g];
+  const unsigned long long b = a.offsets[q0] - a.out_base;
+  const unsigned long long n = a.offsets[q1] + a.counts[q1] - a.out_base - b;
+  unsigned long long *keys = a.keys + b;
+  for (unsigned long long i = 0; i < n; ++i)
+    keys[i] = ((unsigned long long)a.score[b + i] << 32) | (uint32_t)i;
+  stdsort::Sort(keys, (long)n, ScoreDescending());
+  uint32_t *sid_out = a.sel_sid + (size_t)g * a.cap;
+  uint32_t *cand_out = a.sel_cand + (size_t)g * a.cap;
+  uint32_t count = 0;
+  for (unsigned long long i = 0; i < n; ++i) {
+    const unsigned long long c = b + (uint32_t)keys[i];
+    const uint32_t sid = SubjectOf(a.subj_start, a.nsubj, a.dblen, a.end[c]);
+    bool seen = false;
+    for (uint32_t k = 0; k < count; ++k) seen |= sid_out[k] == sid;
+    if (!seen) {
+      sid_out[count] = sid;
+      cand_out[count] = (uint32_t)c;
+      a.tb_qid[(size_t)g * a.cap + count] = a.cand_qid[a.out_base + c];
+      a.tb_end[(size_t)g * a.cap + count] = a.end[c];
+      ++count;
+    }
+    if (count >= a.best) break;
+  }
+  a.sel_count[g] = count;
+  for (uint32_t k = count; k < a.cap; ++k) a.tb_qid[(size_t)g * a.cap + k] = 0xFFFFFFFFu;
+}
+
+// One 20-byte record per selected hit, subject-relative like the reference's
+// rebase after TraceBack (aligner.cpp:710-716).
+struct SlotHit {
+  uint32_t sid, score, start, end, ml;
+};
+
+__global__ void k_finalize(const uint32_t *sel_count, const uint32_t *sel_cand,
+                           const uint32_t *sel_sid, const uint32_t *score, const uint32_t *end,
+                           const uint32_t *tb_start, const uint32_t *tb_ml,
+                           const uint32_t *subj_start, uint32_t ng, uint32_t cap, SlotHit *out) {
+  const size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= (size_t)ng * cap) return;
+  const uint32_t g = (uint32_t)(s / cap), k = (uint32_t)(s - (size_t)g * cap);
+  if (k >= sel_count[g]) return;
+  const uint32_t c = sel_cand[s], sid = sel_sid[s], pos = subj_start[sid];
+  out[s] = SlotHit{sid, score[c], tb_start[s] - pos, end[c] - pos, tb_ml[s]};
 }
 
 }  // namespace kern
