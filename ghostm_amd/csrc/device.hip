@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <climits>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -92,7 +93,7 @@ struct DeviceModule::Impl {
   int h_matrix[32 * 32] = {0};
   DevBuf mat_k2, mat_tb;
   // K1 work
-  DevBuf counts, nelem, slots, offsets, qlist, gbuf, gbuf_off;
+  DevBuf counts, nelem, slots, offsets, qlist, gbuf, gbuf_off, list_beg, list_len;
   DevBuf cand_start, cand_qid;
   uint64_t ncand = 0;
   // K2 work
@@ -126,9 +127,10 @@ void DeviceModule::Bind(int device) {
   stream_ = s;
   HIP_CHECK(hipEventCreate(&impl_->ev0));
   HIP_CHECK(hipEventCreate(&impl_->ev1));
-  HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_seed<false>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                2 * kern::kSeedLdsCap * 4));
+  HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_seed<1024, 16384, false>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 16384 * 4));
+  HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_seed<512, 8192, false>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 8192 * 4));
   device_ = device;
 }
 
@@ -240,6 +242,30 @@ static float ElapsedMs(hipEvent_t a, hipEvent_t b) {
   return ms;
 }
 
+// K1 size classes: (threads, LDS bins per buffer). Bigger queries get bigger
+// workgroups; the last class merges in global memory.
+struct SeedClass {
+  uint32_t block, cap;
+};
+static const SeedClass kSeedClasses[] = {{256, 4096}, {512, 8192}, {1024, 16384}, {1024, 0}};
+
+template <uint32_t B, uint32_t C, bool G>
+static void LaunchSeed(const kern::SeedArgs &a, uint32_t items, hipStream_t s) {
+  const size_t lds = G ? 0 : (size_t)2 * C * 4;
+  hipLaunchKernelGGL((kern::k_seed<B, C, G>), dim3(items), dim3(B), lds, s, a);
+}
+
+static void LaunchSeedClass(int cls, const kern::SeedArgs &a, uint32_t items, hipStream_t s) {
+  if (items == 0) return;
+  switch (cls) {
+    case 0: LaunchSeed<256, 4096, false>(a, items, s); break;
+    case 1: LaunchSeed<512, 8192, false>(a, items, s); break;
+    case 2: LaunchSeed<1024, 16384, false>(a, items, s); break;
+    default: LaunchSeed<1024, 1, true>(a, items, s); break;
+  }
+  HIP_CHECK(hipGetLastError());
+}
+
 uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
                             std::vector<uint32_t> *counts, std::vector<uint64_t> *offsets) {
   Impl &I = *impl_;
@@ -248,7 +274,7 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
   offsets->assign(nq, 0);
   I.ncand = 0;
   if (nq == 0) return 0;
-  const uint32_t seed_len = [](uint32_t s) { uint32_t n = 0; for (; s; s >>= 1) ++n; return n; }(cfg.seed_mask);
+  const uint32_t seed_len = SeedLength(cfg.seed_mask);
   if (seed_len == 0 || seed_len > q->L) return 0;
   if (cfg.shift == 0) throw Error("shift size must be positive");
   const uint32_t nlists = (q->L - seed_len) / cfg.shift + 1;
@@ -259,112 +285,144 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
   I.nelem.Reserve((size_t)nq * 4);
   I.slots.Reserve((size_t)nq * kSlotCap * 4);
   I.offsets.Reserve((size_t)nq * 8);
-  HIP_CHECK(hipMemsetAsync(I.nelem.p, 0, (size_t)nq * 4, S(stream_)));
-
-  kern::SeedArgs a{};
-  a.qseq = q->seq.as<uint8_t>();
-  a.L = q->L;
-  a.keys_count = d->kc.as<uint32_t>();
-  a.positions = d->pos.as<uint32_t>();
-  a.seed_mask = cfg.seed_mask;
-  a.nlists = nlists;
-  a.shift = cfg.shift;
-  a.log_region = cfg.log_region;
-  a.threshold = cfg.threshold;
-  a.counts = I.counts.as<uint32_t>();
-  a.nelem = I.nelem.as<uint32_t>();
-  a.slots = I.slots.as<uint32_t>();
-  a.slot_cap = kSlotCap;
-  const size_t lds = 2 * kern::kSeedLdsCap * 4;
-
+  I.list_beg.Reserve((size_t)nq * nlists * 4);
+  I.list_len.Reserve((size_t)nq * nlists * 4);
   HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
-  // pass 1: every query, LDS merge, candidates into per-query slots
-  hipLaunchKernelGGL(kern::k_seed<false>, dim3(nq), dim3(kern::kSeedBlock), lds, S(stream_), a);
+  HIP_CHECK(hipMemsetAsync(I.counts.p, 0, (size_t)nq * 4, S(stream_)));
+
+  // K1a: list segments + bin count per query
+  kern::SeedListArgs la{};
+  la.qseq = q->seq.as<uint8_t>();
+  la.L = q->L;
+  la.nq = nq;
+  la.keys_count = d->kc.as<uint32_t>();
+  la.positions = d->pos.as<uint32_t>();
+  la.seed_mask = cfg.seed_mask;
+  la.nlists = nlists;
+  la.shift = cfg.shift;
+  la.list_beg = I.list_beg.as<uint32_t>();
+  la.list_len = I.list_len.as<uint32_t>();
+  la.nbins = I.nelem.as<uint32_t>();
+  hipLaunchKernelGGL(kern::k_seed_lists, dim3((nq + 3) / 4), dim3(256), 0, S(stream_), la);
   HIP_CHECK(hipGetLastError());
-  std::vector<uint32_t> nel(nq);
-  HIP_CHECK(hipMemcpyAsync(counts->data(), I.counts.p, (size_t)nq * 4, hipMemcpyDeviceToHost, S(stream_)));
-  HIP_CHECK(hipMemcpyAsync(nel.data(), I.nelem.p, (size_t)nq * 4, hipMemcpyDeviceToHost, S(stream_)));
+  std::vector<uint32_t> nbins(nq);
+  HIP_CHECK(hipMemcpyAsync(nbins.data(), I.nelem.p, (size_t)nq * 4, hipMemcpyDeviceToHost, S(stream_)));
   HIP_CHECK(hipStreamSynchronize(S(stream_)));
 
-  // pass 2: queries whose bins exceed LDS -> global merge buffers (count only)
-  std::vector<uint32_t> big, wide;
+  // size classes (queries without any position keep count 0)
+  std::vector<uint32_t> cls[4];
   std::vector<unsigned long long> goff;
   unsigned long long gtotal = 0;
   uint64_t bins_total = 0;
   for (uint32_t i = 0; i < nq; ++i) {
-    if ((*counts)[i] == kern::kOverflow) {
-      big.push_back(i);
+    const uint32_t n = nbins[i];
+    bins_total += n;
+    if (n == 0) continue;
+    int c = 3;
+    for (int k = 0; k < 3; ++k)
+      if (n <= kSeedClasses[k].cap) { c = k; break; }
+    cls[c].push_back(i);
+    if (c == 3) {
       goff.push_back(gtotal);
-      gtotal += 2ull * nel[i];
+      gtotal += 2ull * n;
     }
   }
-  auto run_global = [&](bool write) {
-    if (big.empty()) return;
-    I.qlist.Reserve(big.size() * 4);
-    I.gbuf_off.Reserve(goff.size() * 8);
+  size_t list_total = 0;
+  for (auto &v : cls) list_total += v.size();
+  I.qlist.Reserve(list_total * 4 + 4);
+  std::vector<uint32_t> pass1;  // outlives the async copy (synchronised below)
+  pass1.reserve(list_total);
+  for (auto &v : cls) pass1.insert(pass1.end(), v.begin(), v.end());
+  if (!pass1.empty())
+    HIP_CHECK(hipMemcpyAsync(I.qlist.p, pass1.data(), pass1.size() * 4, hipMemcpyHostToDevice, S(stream_)));
+  if (gtotal) {
     I.gbuf.Reserve(gtotal * 4);
-    HIP_CHECK(hipMemcpyAsync(I.qlist.p, big.data(), big.size() * 4, hipMemcpyHostToDevice, S(stream_)));
+    I.gbuf_off.Reserve(goff.size() * 8);
     HIP_CHECK(hipMemcpyAsync(I.gbuf_off.p, goff.data(), goff.size() * 8, hipMemcpyHostToDevice, S(stream_)));
-    kern::SeedArgs b = a;
-    b.query_list = I.qlist.as<uint32_t>();
-    b.gbuf = I.gbuf.as<uint32_t>();
-    b.gbuf_off = I.gbuf_off.as<unsigned long long>();
-    b.slots = nullptr;
-    if (write) {
-      b.offsets = I.offsets.as<unsigned long long>();
-      b.out_start = I.cand_start.as<uint32_t>();
-      b.out_qid = I.cand_qid.as<uint32_t>();
-    }
-    hipLaunchKernelGGL(kern::k_seed<true>, dim3((uint32_t)big.size()), dim3(kern::kSeedBlock), 0,
-                       S(stream_), b);
-    HIP_CHECK(hipGetLastError());
-  };
-  if (!big.empty()) {
-    run_global(false);
-    std::vector<uint32_t> c2(nq);
-    HIP_CHECK(hipMemcpyAsync(c2.data(), I.counts.p, (size_t)nq * 4, hipMemcpyDeviceToHost, S(stream_)));
-    HIP_CHECK(hipStreamSynchronize(S(stream_)));
-    for (uint32_t i : big) (*counts)[i] = c2[i];
   }
+
+  kern::SeedArgs a{};
+  a.positions = d->pos.as<uint32_t>();
+  a.nlists = nlists;
+  a.shift = cfg.shift;
+  a.log_region = cfg.log_region;
+  a.threshold = cfg.threshold;
+  a.list_beg = I.list_beg.as<uint32_t>();
+  a.list_len = I.list_len.as<uint32_t>();
+  a.counts = I.counts.as<uint32_t>();
+  a.slots = I.slots.as<uint32_t>();
+  a.slot_cap = kSlotCap;
+  a.gbuf = I.gbuf.as<uint32_t>();
+  a.gbuf_off = I.gbuf_off.as<unsigned long long>();
+  // K1b pass 1: every class, candidates into per-query slots (largest first)
+  {
+    size_t at = list_total;
+    for (int c = 3; c >= 0; --c) {
+      at -= cls[c].size();
+      kern::SeedArgs b = a;
+      b.query_list = I.qlist.as<uint32_t>() + at;
+      LaunchSeedClass(c, b, (uint32_t)cls[c].size(), S(stream_));
+    }
+  }
+  HIP_CHECK(hipMemcpyAsync(counts->data(), I.counts.p, (size_t)nq * 4, hipMemcpyDeviceToHost, S(stream_)));
+  HIP_CHECK(hipStreamSynchronize(S(stream_)));
+
   uint64_t total = 0;
+  std::vector<uint32_t> wide[4];
+  std::vector<unsigned long long> wide_goff;
   for (uint32_t i = 0; i < nq; ++i) {
     (*offsets)[i] = total;
     total += (*counts)[i];
-    if ((*counts)[i] > kSlotCap && nel[i] == 0) wide.push_back(i);
-    bins_total += nel[i];
+  }
+  for (int c = 0; c < 4; ++c) {
+    size_t gi = 0;
+    for (uint32_t qi : cls[c]) {
+      if ((*counts)[qi] > kSlotCap) {
+        wide[c].push_back(qi);
+        if (c == 3) wide_goff.push_back(goff[gi]);
+      }
+      ++gi;
+    }
   }
   I.ncand = total;
   I.cand_start.Reserve(total * 4 + 4);
   I.cand_qid.Reserve(total * 4 + 4);
   HIP_CHECK(hipMemcpyAsync(I.offsets.p, offsets->data(), (size_t)nq * 8, hipMemcpyHostToDevice, S(stream_)));
-  // pass 3: slot -> compact
+  // slot -> compact
   hipLaunchKernelGGL(kern::k_compact, dim3((nq + 3) / 4), dim3(256), 0, S(stream_),
-                     I.slots.as<uint32_t>(), kSlotCap, I.counts.as<uint32_t>(),
-                     I.nelem.as<uint32_t>(), I.offsets.as<unsigned long long>(), nq,
-                     I.cand_start.as<uint32_t>(), I.cand_qid.as<uint32_t>());
+                     I.slots.as<uint32_t>(), kSlotCap, I.counts.as<uint32_t>(), (const uint8_t *)nullptr,
+                     I.offsets.as<unsigned long long>(), nq, I.cand_start.as<uint32_t>(),
+                     I.cand_qid.as<uint32_t>());
   HIP_CHECK(hipGetLastError());
-  // pass 4: queries with more candidates than a slot -> rerun straight into place
-  if (!wide.empty()) {
-    I.qlist.Reserve(wide.size() * 4);
-    HIP_CHECK(hipMemcpyAsync(I.qlist.p, wide.data(), wide.size() * 4, hipMemcpyHostToDevice, S(stream_)));
-    kern::SeedArgs b = a;
-    b.query_list = I.qlist.as<uint32_t>();
-    b.slots = nullptr;
-    b.offsets = I.offsets.as<unsigned long long>();
-    b.out_start = I.cand_start.as<uint32_t>();
-    b.out_qid = I.cand_qid.as<uint32_t>();
-    hipLaunchKernelGGL(kern::k_seed<false>, dim3((uint32_t)wide.size()), dim3(kern::kSeedBlock), lds,
-                       S(stream_), b);
-    HIP_CHECK(hipGetLastError());
-    HIP_CHECK(hipStreamSynchronize(S(stream_)));
+  // pass 2: queries with more candidates than a slot, written straight into place
+  size_t nwide = 0;
+  for (auto &v : wide) nwide += v.size();
+  std::vector<uint32_t> all;  // outlives the async copy
+  if (nwide) {
+    all.reserve(nwide);
+    for (auto &v : wide) all.insert(all.end(), v.begin(), v.end());
+    I.qlist.Reserve(all.size() * 4);
+    HIP_CHECK(hipMemcpyAsync(I.qlist.p, all.data(), all.size() * 4, hipMemcpyHostToDevice, S(stream_)));
+    if (!wide_goff.empty())
+      HIP_CHECK(hipMemcpyAsync(I.gbuf_off.p, wide_goff.data(), wide_goff.size() * 8, hipMemcpyHostToDevice,
+                               S(stream_)));
+    size_t at = 0;
+    for (int c = 0; c < 4; ++c) {
+      kern::SeedArgs b = a;
+      b.query_list = I.qlist.as<uint32_t>() + at;
+      b.slots = nullptr;
+      b.offsets = I.offsets.as<unsigned long long>();
+      b.out_start = I.cand_start.as<uint32_t>();
+      b.out_qid = I.cand_qid.as<uint32_t>();
+      LaunchSeedClass(c, b, (uint32_t)wide[c].size(), S(stream_));
+      at += wide[c].size();
+    }
   }
-  // pass 5: LDS-overflow queries, written from global merge buffers
-  run_global(true);
   HIP_CHECK(hipEventRecord(I.ev1, S(stream_)));
   times_.seed += ElapsedMs(I.ev0, I.ev1) * 1e-3;
-  // algorithmic bytes: query record + 2 CSR words per list + positions + outputs
-  (void)bins_total;
-  times_.seed_bytes += (uint64_t)nq * (q->L + 8ull * nlists + 4) + total * 8ull;
+  // algorithmic bytes: query record + 2 CSR words per list + one u32 per
+  // position + 8 bytes (start, query) per candidate
+  times_.seed_bytes += (uint64_t)nq * (q->L + 8ull * nlists) + bins_total * 4ull + total * 8ull;
   return total;
 }
 
@@ -381,7 +439,13 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
   if (n == 0) return;
   if (gap.ext > 0) throw Error("positive gap extension score is not supported");
   const Layout lay = ChooseLayout(q->L, base);
-  const uint32_t per_block = (kern::kScoreBlock / 64) * lay.gpw;
+  // packed int16 path (two candidates per lane) whenever every value fits
+  int max_abs = 0;
+  for (int v : I.h_matrix) max_abs = std::max(max_abs, v < 0 ? -v : v);
+  const char *force = getenv("GHOSTM_K2");
+  const bool packed = !(force && strcmp(force, "int32") == 0) && gap.open <= 0 && gap.ext <= 0 &&
+                      -gap.open < 32000 && -gap.ext < 32000 && (int64_t)q->L * max_abs < 30000;
+  const uint32_t per_block = (kern::kScoreBlock / 64) * lay.gpw * (packed ? 2 : 1);
   // tasks: runs of <= per_block consecutive candidates spanning <= Qmax queries
   std::vector<kern::ScoreTask> tasks;
   tasks.reserve(n / per_block + (q_end - q_first) / kern::kScoreQmax + 2);
@@ -438,13 +502,22 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
   I.counters.Reserve(16);
   HIP_CHECK(hipMemsetAsync(I.counters.p, 0, 16, S(stream_)));
   a.cells = I.counters.as<unsigned long long>();
-  const size_t lds = (size_t)kern::kScoreQmax * kern::kProfRows * (lay.Lpad + 4) * 4;
+  const size_t lds = packed ? (size_t)kern::kScoreQmax * kern::kProfRows * (lay.Lpad + 8) * 2
+                            : (size_t)kern::kScoreQmax * kern::kProfRows * (lay.Lpad + 4) * 4;
   HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
   const dim3 grid((uint32_t)tasks.size()), block(kern::kScoreBlock);
-  switch (lay.S) {
-    case 32: hipLaunchKernelGGL(kern::k_score<32>, grid, block, lds, S(stream_), a); break;
-    case 16: hipLaunchKernelGGL(kern::k_score<16>, grid, block, lds, S(stream_), a); break;
-    default: hipLaunchKernelGGL(kern::k_score<8>, grid, block, lds, S(stream_), a); break;
+  if (packed) {
+    switch (lay.S) {
+      case 32: hipLaunchKernelGGL(kern::k_score16<32>, grid, block, lds, S(stream_), a); break;
+      case 16: hipLaunchKernelGGL(kern::k_score16<16>, grid, block, lds, S(stream_), a); break;
+      default: hipLaunchKernelGGL(kern::k_score16<8>, grid, block, lds, S(stream_), a); break;
+    }
+  } else {
+    switch (lay.S) {
+      case 32: hipLaunchKernelGGL(kern::k_score<32>, grid, block, lds, S(stream_), a); break;
+      case 16: hipLaunchKernelGGL(kern::k_score<16>, grid, block, lds, S(stream_), a); break;
+      default: hipLaunchKernelGGL(kern::k_score<8>, grid, block, lds, S(stream_), a); break;
+    }
   }
   HIP_CHECK(hipGetLastError());
   HIP_CHECK(hipEventRecord(I.ev1, S(stream_)));

@@ -32,20 +32,63 @@ constexpr uint32_t kPadCode = 31;      // unused residue code: query padding row
 constexpr int kNeg = -30000;           // score of a padding row (keeps it at 0)
 
 // ------------------------------------------------------------------ K1 seed
-constexpr uint32_t kSeedBlock = 512;
-constexpr uint32_t kSeedLdsCap = 16384;   // bins per LDS buffer (2 buffers)
+// K1a k_seed_lists: one wave per query, lane j = k-mer list j: key -> CSR range,
+//     positions before the list's diagonal origin j*shift dropped; writes the
+//     list segments and the query's bin count (massively parallel: the dependent
+//     index lookups of 1M queries overlap).
+// K1b k_seed<BLOCK, CAP, GBUF>: one workgroup per query (by size class): gather
+//     the bins (one load per position), mark in-list repeats, merge-path tree in
+//     LDS (or global buffers for oversized queries), run-length emission.
 constexpr uint32_t kMaxLists = 128;
 constexpr uint32_t kOverflow = 0xFFFFFFFFu;
 
-struct SeedArgs {
+struct SeedListArgs {
   const uint8_t *qseq;
-  uint32_t L;
+  uint32_t L, nq;
   const uint32_t *keys_count;
   const uint32_t *positions;
-  uint32_t seed_mask, nlists, shift, log_region, threshold;
-  const uint32_t *query_list;     // null: query = blockIdx.x
+  uint32_t seed_mask, nlists, shift;
+  uint32_t *list_beg;             // [nq * nlists]
+  uint32_t *list_len;             // [nq * nlists]
+  uint32_t *nbins;                // [nq]
+};
+
+__global__ __launch_bounds__(256) void k_seed_lists(SeedListArgs a) {
+  const uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63;
+  if (q >= a.nq) return;
+  const uint8_t *qs = a.qseq + (size_t)q * a.L;
+  uint32_t total = 0;
+  for (uint32_t j = lane; j < a.nlists; j += 64) {
+    const uint32_t d0 = j * a.shift;
+    uint32_t key = 0, t = 0;
+    for (uint32_t s = a.seed_mask; s; s >>= 1, ++t)
+      if (s & 1u) key = (key << 5) | qs[d0 + t];
+    const uint32_t b = a.keys_count[key], e = a.keys_count[key + 1];
+    uint32_t lo = b;
+    if (b < e && a.positions[b] < d0) {  // rare: hits in the first j*shift residues
+      uint32_t hi = e;
+      lo = b + 1;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a.positions[mid] < d0) lo = mid + 1; else hi = mid;
+      }
+    }
+    a.list_beg[(size_t)q * a.nlists + j] = lo;
+    a.list_len[(size_t)q * a.nlists + j] = e - lo;
+    total += e - lo;
+  }
+  for (int d = 32; d > 0; d >>= 1) total += __shfl_xor(total, d);
+  if (lane == 0) a.nbins[q] = total;
+}
+
+struct SeedArgs {
+  const uint32_t *positions;
+  uint32_t nlists, shift, log_region, threshold;
+  const uint32_t *list_beg;       // from K1a
+  const uint32_t *list_len;
+  const uint32_t *query_list;     // queries of this size class
   uint32_t *counts;               // [nq] candidates per query
-  uint32_t *nelem;                // [nq] bins of a query that did not fit LDS
   uint32_t *slots;                // slot mode: candidates at q*slot_cap
   uint32_t slot_cap;
   const unsigned long long *offsets;  // offset mode: candidates at offsets[q]
@@ -98,40 +141,40 @@ __device__ inline bool EmitRun(const uint32_t *S, uint32_t n, uint32_t i, uint32
   return c0 + c1 >= threshold;
 }
 
-template <bool GBUF>
-__global__ __launch_bounds__(kSeedBlock) void k_seed(SeedArgs a) {
+// Largest j in [0, hi] with off[j] <= x (off non-decreasing).
+__device__ inline uint32_t UpperIndex(const uint32_t *off, uint32_t hi, uint32_t x) {
+  uint32_t lo = 0;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) >> 1;
+    if (off[mid] <= x) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+template <uint32_t BLOCK, uint32_t CAP, bool GBUF>
+__global__ __launch_bounds__(BLOCK) void k_seed(SeedArgs a) {
   __shared__ uint32_t s_beg[kMaxLists];
   __shared__ uint32_t s_off[kMaxLists + 1];
-  __shared__ uint32_t s_part[kSeedBlock / 64];
+  __shared__ uint32_t s_part[BLOCK / 64];
   __shared__ uint32_t s_total;
   extern __shared__ __attribute__((aligned(16))) uint32_t s_buf[];
 
   const uint32_t item = blockIdx.x;
-  const uint32_t q = a.query_list ? a.query_list[item] : item;
+  const uint32_t q = a.query_list[item];
   const uint32_t tid = threadIdx.x;
-  const uint8_t *qs = a.qseq + (size_t)q * a.L;
+  const uint32_t nl = a.nlists;
 
-  // 1. one k-mer list per seed offset j*shift; drop positions before the offset
+  // 1. list segments (K1a) and their offsets in the block's bin array
   uint32_t len = 0;
-  if (tid < a.nlists) {
-    const uint32_t d0 = tid * a.shift;
-    uint32_t key = 0, t = 0;
-    for (uint32_t s = a.seed_mask; s; s >>= 1, ++t)
-      if (s & 1u) key = (key << 5) | qs[d0 + t];
-    const uint32_t b = a.keys_count[key], e = a.keys_count[key + 1];
-    uint32_t lo = b, hi = e;
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (a.positions[mid] < d0) lo = mid + 1; else hi = mid;
-    }
-    s_beg[tid] = lo;
-    len = e - lo;
+  if (tid < nl) {
+    s_beg[tid] = a.list_beg[(size_t)q * nl + tid];
+    len = a.list_len[(size_t)q * nl + tid];
   }
   const uint32_t excl = BlockExclusiveScan(len, s_part, &s_total);
-  if (tid < a.nlists) s_off[tid] = excl;
-  if (tid == 0) s_off[a.nlists] = s_total;
+  if (tid < nl) s_off[tid] = excl;
+  if (tid == 0) s_off[nl] = s_total;
   __syncthreads();
-  const uint32_t n = s_off[a.nlists];
+  const uint32_t n = s_off[nl];
   if (n == 0) {
     if (tid == 0) a.counts[q] = 0;
     return;
@@ -141,32 +184,46 @@ __global__ __launch_bounds__(kSeedBlock) void k_seed(SeedArgs a) {
     buf0 = a.gbuf + a.gbuf_off[item];
     buf1 = buf0 + n;
   } else {
-    if (n > kSeedLdsCap) {
-      if (tid == 0) { a.counts[q] = kOverflow; a.nelem[q] = n; }
-      return;
-    }
     buf0 = s_buf;
-    buf1 = s_buf + kSeedLdsCap;
+    buf1 = s_buf + CAP;
   }
 
-  // 2. gather: key = bin << 1 | (bin repeats the previous bin of the same list)
-  const uint32_t nl = a.nlists;
-  for (uint32_t i = tid; i < n; i += kSeedBlock) {
-    uint32_t lo = 0, hi = nl - 1;
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi + 1) >> 1;
-      if (s_off[mid] <= i) lo = mid; else hi = mid - 1;
+  // 2. gather: buf1 = bin | list-start flag, four positions in flight per thread
+  for (uint32_t base = tid; base < n; base += 4 * BLOCK) {
+    uint32_t idx[4], d0[4], st[4], pos[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t i = base + u * BLOCK;
+      idx[u] = 0;
+      d0[u] = 0;
+      st[u] = 0;
+      if (i < n) {
+        const uint32_t j = UpperIndex(s_off, nl - 1, i);
+        const uint32_t r = i - s_off[j];
+        idx[u] = s_beg[j] + r;
+        d0[u] = j * a.shift;
+        st[u] = r == 0 ? 0x80000000u : 0u;
+      }
     }
-    const uint32_t r = i - s_off[lo], idx = s_beg[lo] + r, d0 = lo * a.shift;
-    const uint32_t bin = (a.positions[idx] - d0) >> a.log_region;
-    uint32_t dup = 0;
-    if (r > 0) dup = ((a.positions[idx - 1] - d0) >> a.log_region) == bin;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) pos[u] = (base + u * BLOCK < n) ? a.positions[idx[u]] : 0u;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t i = base + u * BLOCK;
+      if (i < n) buf1[i] = ((pos[u] - d0[u]) >> a.log_region) | st[u];
+    }
+  }
+  __syncthreads();
+  // key = bin << 1 | (bin repeats the previous bin of the same list)
+  for (uint32_t i = tid; i < n; i += BLOCK) {
+    const uint32_t v = buf1[i], bin = v & 0x7FFFFFFFu;
+    const uint32_t dup = (!(v >> 31) && (buf1[i - 1] & 0x7FFFFFFFu) == bin) ? 1u : 0u;
     buf0[i] = (bin << 1) | dup;
   }
 
   // 3. merge-path tree: segments of w lists are merged pairwise per round
   uint32_t *src = buf0, *dst = buf1;
-  const uint32_t per = (n + kSeedBlock - 1) / kSeedBlock;
+  const uint32_t per = (n + BLOCK - 1) / BLOCK;
   for (uint32_t w = 1; w < nl; w <<= 1) {
     __syncthreads();
     const uint32_t npairs = (nl + 2 * w - 1) / (2 * w);
@@ -190,10 +247,17 @@ __global__ __launch_bounds__(kSeedBlock) void k_seed(SeedArgs a) {
         if (A[mid] <= B[d0 - 1 - mid]) l2 = mid + 1; else h2 = mid;
       }
       uint32_t ia = l2, ib = d0 - l2;
+      uint32_t va = ia < na ? A[ia] : 0xFFFFFFFFu, vb = ib < nb ? B[ib] : 0xFFFFFFFFu;
       for (uint32_t d = d0; d < d1; ++d) {
-        uint32_t v;
-        if (ib >= nb || (ia < na && A[ia] <= B[ib])) v = A[ia++]; else v = B[ib++];
-        dst[P0 + d] = v;
+        if (ib >= nb || (ia < na && va <= vb)) {
+          dst[P0 + d] = va;
+          ++ia;
+          va = ia < na ? A[ia] : 0xFFFFFFFFu;
+        } else {
+          dst[P0 + d] = vb;
+          ++ib;
+          vb = ib < nb ? B[ib] : 0xFFFFFFFFu;
+        }
       }
       g = P0 + d1;
     }
@@ -248,12 +312,12 @@ __global__ __launch_bounds__(kSeedBlock) void k_seed(SeedArgs a) {
 
 // Slot -> compact copy for queries whose candidates fit their slot.
 __global__ void k_compact(const uint32_t *slots, uint32_t slot_cap, const uint32_t *counts,
-                          const uint32_t *nelem, const unsigned long long *offsets,
+                          const uint8_t *in_slot, const unsigned long long *offsets,
                           uint32_t nq, uint32_t *out_start, uint32_t *out_qid) {
   const uint32_t q = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   if (q >= nq) return;
   const uint32_t c = counts[q];
-  if (nelem[q] != 0 || c > slot_cap) return;
+  if ((in_slot && !in_slot[q]) || c > slot_cap) return;
   const unsigned long long o = offsets[q];
   for (uint32_t i = threadIdx.x & 63; i < c; i += 64) {
     out_start[o + i] = slots[(size_t)q * slot_cap + i];
@@ -395,6 +459,175 @@ __global__ __launch_bounds__(kScoreBlock) void k_score(ScoreArgs a) {
     a.end_out[cand - a.out_base] = off + (uint32_t)C;
   }
   WaveAddCells(a.cells, (valid && i == 0) ? (unsigned long long)ncols * a.L : 0ull);
+}
+
+// ------------------------------------------------------------------ K2 packed
+// k_score16: the same lane-group DP with TWO candidates per lane, one in each
+// 16-bit half of every register (v_pk_* ops: one instruction advances two
+// cells). The two candidates read different DB residues, so their profile
+// values are fetched separately and interleaved with v_perm_b32. Gap states are
+// kept clamped at >= 0 (exact: E and F only matter once positive, h >= 0), so
+// the open/extend updates are unsigned saturating subtractions. Used when every
+// score fits int16 (L * max matrix entry < 30000) and gap penalties are >= 0.
+typedef short sh2 __attribute__((ext_vector_type(2)));
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+constexpr short kNeg16 = -8000;
+
+__device__ inline sh2 S2(uint32_t v) { return __builtin_bit_cast(sh2, v); }
+__device__ inline us2 U2(uint32_t v) { return __builtin_bit_cast(us2, v); }
+__device__ inline uint32_t W(sh2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ inline uint32_t W(us2 v) { return __builtin_bit_cast(uint32_t, v); }
+
+// lane l receives lane l-1's value (lane 0: 0) — DPP wave_shr:1, a VALU op with
+// no LDS round trip (the group-boundary lanes overwrite it with their own zeros)
+__device__ inline uint32_t ShiftUp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
+}
+
+template <int S>
+__global__ __launch_bounds__(kScoreBlock) void k_score16(ScoreArgs a) {
+  extern __shared__ __attribute__((aligned(16))) short s_prof16[];
+  const ScoreTask t = a.tasks[blockIdx.x];
+  const uint32_t RS = a.Lpad + 8;  // int16 elements; 16-byte pad spreads LDS banks
+
+  const uint32_t per_slot = kProfRows * a.Lpad;
+  const uint32_t total = t.q_count * per_slot;
+  for (uint32_t e = threadIdx.x; e < total; e += kScoreBlock) {
+    const uint32_t slot = e / per_slot, rem = e - slot * per_slot;
+    const uint32_t c = rem / a.Lpad, r = rem - c * a.Lpad;
+    short v = kNeg16;
+    if (r >= a.pad)
+      v = c < 25 ? (short)a.mat[c * 32 + a.qseq[(size_t)(t.q_first + slot) * a.L + (r - a.pad)]] : (short)0;
+    s_prof16[(slot * kProfRows + c) * RS + r] = v;
+  }
+  __syncthreads();
+
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t g = lane / a.G, i = lane - g * a.G;
+  const uint32_t pair = wave * a.gpw + g;
+  const bool in_group = g < a.gpw;
+  const bool vA = in_group && 2 * pair < t.count;
+  const bool vB = in_group && 2 * pair + 1 < t.count;
+  const unsigned long long cA = t.begin + 2 * pair, cB = cA + 1;
+  uint32_t slotA = 0, slotB = 0, offA = 0, offB = 0, wA = 0, wB = 0;
+  if (vA) {
+    slotA = a.cand_qid[cA] - t.q_first;
+    int o = (int)(a.cand_start[cA] - a.extend);
+    offA = o < 0 ? 0u : (uint32_t)o;
+    wA = a.base;
+    if (offA + wA > a.dblen) wA = a.dblen - offA;
+  }
+  if (vB) {
+    slotB = a.cand_qid[cB] - t.q_first;
+    int o = (int)(a.cand_start[cB] - a.extend);
+    offB = o < 0 ? 0u : (uint32_t)o;
+    wB = a.base;
+    if (offB + wB > a.dblen) wB = a.dblen - offB;
+  }
+  const short *profA = s_prof16 + slotA * kProfRows * RS + i * S;
+  const short *profB = s_prof16 + slotB * kProfRows * RS + i * S;
+  const us2 gopen = U2((uint32_t)(-a.open) * 0x10001u);
+  const us2 gext = U2((uint32_t)(-a.ext) * 0x10001u);
+
+  uint32_t H[S], E[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) { H[k] = 0; E[k] = 0; }
+  int bestA = 0, bestB = 0, colA = 0, colB = 0;
+  uint32_t ncols = 0;
+  uint32_t hout = 0, fout = 0, hprev = 0;
+  int j = -(int)i;
+  uint32_t nA = kSeqEnd, nB = kSeqEnd;
+  if (j >= 0 && (uint32_t)j < wA) nA = a.db[offA + j];
+  if (j >= 0 && (uint32_t)j < wB) nB = a.db[offB + j];
+  const uint32_t steps = a.base + a.G - 1;
+  for (uint32_t step = 0; step < steps; ++step, ++j) {
+    uint32_t hin = ShiftUp(hout), fin = ShiftUp(fout);
+    if (i == 0) { hin = 0; fin = 0; }
+    const uint32_t diag0 = hprev;
+    hprev = hin;
+    const uint32_t rA = nA, rB = nB;
+    nA = kSeqEnd;
+    nB = kSeqEnd;
+    if (j + 1 >= 0 && (uint32_t)(j + 1) < wA) nA = a.db[offA + j + 1];
+    if (j + 1 >= 0 && (uint32_t)(j + 1) < wB) nB = a.db[offB + j + 1];
+    // inactive columns (fill, drain, beyond the window) behave as END: state reset
+    const bool endA = rA == kSeqEnd, endB = rB == kSeqEnd;
+    const short *pA = profA + (rA < 25 ? rA : 25u) * RS;
+    const short *pB = profB + (rB < 25 ? rB : 25u) * RS;
+    uint32_t diag = diag0, F = fin, cm = 0;
+#pragma unroll
+    for (int k = 0; k < S; k += 8) {
+      const uint4 qa = *reinterpret_cast<const uint4 *>(pA + k);
+      const uint4 qb = *reinterpret_cast<const uint4 *>(pB + k);
+      const uint32_t wa[4] = {qa.x, qa.y, qa.z, qa.w}, wb[4] = {qb.x, qb.y, qb.z, qb.w};
+      // diagonal sums of the chunk first, from the previous column's H, so the
+      // row updates below overwrite H in place (no register rotation copies)
+      sh2 s[8];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const uint32_t lo = __builtin_amdgcn_perm(wb[m], wa[m], 0x05040100u);
+        const uint32_t hi = __builtin_amdgcn_perm(wb[m], wa[m], 0x07060302u);
+        s[2 * m] = S2(2 * m == 0 ? diag : H[k + 2 * m - 1]) + S2(lo);
+        s[2 * m + 1] = S2(H[k + 2 * m]) + S2(hi);
+      }
+      diag = H[k + 7];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int r = k + u;
+        const sh2 h = __builtin_elementwise_max(__builtin_elementwise_max(s[u], S2(E[r])), S2(F));
+        H[r] = W(h);
+        const us2 o = __builtin_elementwise_sub_sat(U2(W(h)), gopen);
+        E[r] = W(__builtin_elementwise_max(__builtin_elementwise_sub_sat(U2(E[r]), gext), o));
+        F = W(__builtin_elementwise_max(__builtin_elementwise_sub_sat(U2(F), gext), o));
+      }
+      // column max of the chunk as a tree (a serial max chain stalls on
+      // back-to-back dependent packed ops)
+      const us2 m01 = __builtin_elementwise_max(U2(H[k]), U2(H[k + 1]));
+      const us2 m23 = __builtin_elementwise_max(U2(H[k + 2]), U2(H[k + 3]));
+      const us2 m45 = __builtin_elementwise_max(U2(H[k + 4]), U2(H[k + 5]));
+      const us2 m67 = __builtin_elementwise_max(U2(H[k + 6]), U2(H[k + 7]));
+      const us2 m = __builtin_elementwise_max(__builtin_elementwise_max(m01, m23),
+                                              __builtin_elementwise_max(m45, m67));
+      cm = W(__builtin_elementwise_max(U2(cm), m));
+    }
+    hout = H[S - 1];
+    fout = F;
+    if (__any(endA || endB)) {
+      const uint32_t keep = (endA ? 0xFFFF0000u : 0xFFFFFFFFu) & (endB ? 0x0000FFFFu : 0xFFFFFFFFu);
+#pragma unroll
+      for (int k = 0; k < S; ++k) { H[k] &= keep; E[k] &= keep; }
+      hout &= keep;
+      fout &= keep;
+    }
+    const int cmA = (int)(cm & 0xFFFFu), cmB = (int)(cm >> 16);
+    if (!endA) {
+      if (cmA >= bestA) { bestA = cmA; colA = j; }
+      ++ncols;
+    }
+    if (!endB) {
+      if (cmB >= bestB) { bestB = cmB; colB = j; }
+      ++ncols;
+    }
+  }
+  int BA = bestA, CA = colA, BB = bestB, CB = colB;
+  for (uint32_t k = 1; k < a.G; ++k) {
+    const int src = (int)(g * a.G + k);
+    const int oba = __shfl(bestA, src), oca = __shfl(colA, src);
+    const int obb = __shfl(bestB, src), ocb = __shfl(colB, src);
+    if (oba > BA || (oba == BA && oca > CA)) { BA = oba; CA = oca; }
+    if (obb > BB || (obb == BB && ocb > CB)) { BB = obb; CB = ocb; }
+  }
+  if (i == 0) {
+    if (vA) {
+      a.score_out[cA - a.out_base] = (uint32_t)BA;
+      a.end_out[cA - a.out_base] = offA + (uint32_t)CA;
+    }
+    if (vB) {
+      a.score_out[cB - a.out_base] = (uint32_t)BB;
+      a.end_out[cB - a.out_base] = offB + (uint32_t)CB;
+    }
+  }
+  WaveAddCells(a.cells, (in_group && i == 0) ? (unsigned long long)ncols * a.L : 0ull);
 }
 
 // ------------------------------------------------------------------ K3 traceback

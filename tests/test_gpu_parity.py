@@ -176,3 +176,14 @@ def test_reference_gpu_batching_rule(dataset):
         start += qc
     assert seen == start
     lib.FreeGpu()
+
+
+@pytest.mark.parametrize("ds,var,opts", [("syn_small", "default", []), ("syn_short", "default", []),
+                                         ("syn_small", "r64_pam250", ["-r", "64", "-M", cases.PAM250, "-y", "2"])])
+def test_int32_score_kernel_matches_golden(ds, var, opts, dataset, golden, tmp_path):
+    """The int32 K2 kernel (used when scores may not fit int16) stays covered:
+    forced with GHOSTM_K2=int32 it reproduces the same golden outputs."""
+    d = dataset(ds)
+    text, st = _gpu_text(d, opts, {"GHOSTM_K2": "int32"}, str(tmp_path / "g.out"))
+    (tmp_path / "g.out").write_bytes(text)
+    assert cases.sha256(str(tmp_path / "g.out")) == golden["aln"][f"{ds}/{var}"]["sha256"]
