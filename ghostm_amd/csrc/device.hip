@@ -442,9 +442,14 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
   // packed int16 path (two candidates per lane) whenever every value fits
   int max_abs = 0;
   for (int v : I.h_matrix) max_abs = std::max(max_abs, v < 0 ? -v : v);
+  // encoding: f16 pairs when every score fits the exact-integer range of f16,
+  // else int16 pairs, else int32 (GHOSTM_K2=int32|int16|f16 restricts the choice)
   const char *force = getenv("GHOSTM_K2");
-  const bool packed = !(force && strcmp(force, "int32") == 0) && gap.open <= 0 && gap.ext <= 0 &&
-                      -gap.open < 32000 && -gap.ext < 32000 && (int64_t)q->L * max_abs < 30000;
+  const bool gaps_ok = gap.open <= 0 && gap.ext <= 0 && -gap.open < 2000 && -gap.ext < 2000;
+  const int64_t bound = (int64_t)q->L * max_abs;
+  const bool allow_packed = !(force && strcmp(force, "int32") == 0);
+  const bool half = allow_packed && !(force && strcmp(force, "int16") == 0) && gaps_ok && bound < 2048;
+  const bool packed = allow_packed && gaps_ok && bound < 30000;
   const uint32_t per_block = (kern::kScoreBlock / 64) * lay.gpw * (packed ? 2 : 1);
   // tasks: runs of <= per_block consecutive candidates spanning <= Qmax queries
   std::vector<kern::ScoreTask> tasks;
@@ -508,9 +513,18 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
   const dim3 grid((uint32_t)tasks.size()), block(kern::kScoreBlock);
   if (packed) {
     switch (lay.S) {
-      case 32: hipLaunchKernelGGL(kern::k_score16<32>, grid, block, lds, S(stream_), a); break;
-      case 16: hipLaunchKernelGGL(kern::k_score16<16>, grid, block, lds, S(stream_), a); break;
-      default: hipLaunchKernelGGL(kern::k_score16<8>, grid, block, lds, S(stream_), a); break;
+      case 32:
+        if (half) hipLaunchKernelGGL((kern::k_score16<32, true>), grid, block, lds, S(stream_), a);
+        else hipLaunchKernelGGL((kern::k_score16<32, false>), grid, block, lds, S(stream_), a);
+        break;
+      case 16:
+        if (half) hipLaunchKernelGGL((kern::k_score16<16, true>), grid, block, lds, S(stream_), a);
+        else hipLaunchKernelGGL((kern::k_score16<16, false>), grid, block, lds, S(stream_), a);
+        break;
+      default:
+        if (half) hipLaunchKernelGGL((kern::k_score16<8, true>), grid, block, lds, S(stream_), a);
+        else hipLaunchKernelGGL((kern::k_score16<8, false>), grid, block, lds, S(stream_), a);
+        break;
     }
   } else {
     switch (lay.S) {
@@ -528,6 +542,8 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
   HIP_CHECK(hipStreamSynchronize(S(stream_)));
   times_.score += ElapsedMs(I.ev0, I.ev1) * 1e-3;
   times_.score_launches += 1;
+  times_.score_launches_packed += packed ? 1 : 0;
+  times_.score_launches_half += half ? 1 : 0;
   times_.score_cells += cells;
 }
 

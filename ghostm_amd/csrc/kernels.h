@@ -462,21 +462,30 @@ __global__ __launch_bounds__(kScoreBlock) void k_score(ScoreArgs a) {
 }
 
 // ------------------------------------------------------------------ K2 packed
-// k_score16: the same lane-group DP with TWO candidates per lane, one in each
-// 16-bit half of every register (v_pk_* ops: one instruction advances two
-// cells). The two candidates read different DB residues, so their profile
+// k_score16<S, HALF>: the same lane-group DP with TWO candidates per lane, one in
+// each 16-bit half of every register (VOP3P packed ops: one instruction advances
+// two cells). The two candidates read different DB residues, so their profile
 // values are fetched separately and interleaved with v_perm_b32. Gap states are
-// kept clamped at >= 0 (exact: E and F only matter once positive, h >= 0), so
-// the open/extend updates are unsigned saturating subtractions. Used when every
-// score fits int16 (L * max matrix entry < 30000) and gap penalties are >= 0.
+// kept clamped at >= 0 (exact: E and F only matter once positive, h >= 0).
+//   HALF = false  signed int16 H; the open/extend updates are unsigned saturating
+//                 subtractions. Used when L * max|M| < 30000.
+//   HALF = true   IEEE f16 holding the same integers — exact, since every H, E, F
+//                 is an integer in [0, L * max|M|] <= 2047 and diag + profile is
+//                 either exact or (padding rows) far below zero. gfx950's
+//                 v_pk_maximum3_f16 folds the three-way maxima and the clamp at 0:
+//                 per row add, max3 (H), add (open), add + max3 (E), add + max3 (F)
+//                 = 7 packed ops instead of 8, and the column max is a max3 tree.
 typedef short sh2 __attribute__((ext_vector_type(2)));
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+typedef _Float16 hf2 __attribute__((ext_vector_type(2)));
 constexpr short kNeg16 = -8000;
 
 __device__ inline sh2 S2(uint32_t v) { return __builtin_bit_cast(sh2, v); }
 __device__ inline us2 U2(uint32_t v) { return __builtin_bit_cast(us2, v); }
+__device__ inline hf2 HF(uint32_t v) { return __builtin_bit_cast(hf2, v); }
 __device__ inline uint32_t W(sh2 v) { return __builtin_bit_cast(uint32_t, v); }
 __device__ inline uint32_t W(us2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ inline uint32_t W(hf2 v) { return __builtin_bit_cast(uint32_t, v); }
 
 // lane l receives lane l-1's value (lane 0: 0) — DPP wave_shr:1, a VALU op with
 // no LDS round trip (the group-boundary lanes overwrite it with their own zeros)
@@ -484,21 +493,91 @@ __device__ inline uint32_t ShiftUp(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
 }
 
-template <int S>
+// Packed cell arithmetic of the two encodings. Scores of both encodings are
+// non-negative, so their 16-bit patterns order like their values.
+//
+// END columns (and the inactive fill/drain columns) reset the DP without a
+// branch: in the END column the half's gap penalties become huge, so E and the
+// F chain come out 0 through the max with 0; in the column after it the
+// diagonal term is formed as fma(H, m, profile) with m = 0 for that half, so
+// the END column's H never reaches a score. (The END column's own column max is
+// not counted.)
+template <bool HALF> struct Cells;
+template <> struct Cells<false> {
+  uint32_t gopen, gext;  // positive penalties in both halves
+  struct Step {
+    us2 gopen, gext;
+    uint32_t m;
+  };
+  __device__ Cells(int open, int ext) : gopen((uint32_t)(-open) * 0x10001u), gext((uint32_t)(-ext) * 0x10001u) {}
+  // end / prev_end: 0xFFFF in the halves whose column is / was END
+  __device__ Step At(uint32_t end, uint32_t prev_end) const {
+    return Step{U2(gopen | end), U2(gext | end), 0x00010001u & ~prev_end};
+  }
+  __device__ static uint32_t Diag(uint32_t h, uint32_t m, uint32_t p) { return W(S2(h) * S2(m) + S2(p)); }
+  __device__ static void Row(const Step &st, uint32_t s, uint32_t &H, uint32_t &E, uint32_t &F) {
+    const sh2 h = __builtin_elementwise_max(__builtin_elementwise_max(S2(s), S2(E)), S2(F));
+    H = W(h);
+    const us2 o = __builtin_elementwise_sub_sat(U2(H), st.gopen);
+    E = W(__builtin_elementwise_max(__builtin_elementwise_sub_sat(U2(E), st.gext), o));
+    F = W(__builtin_elementwise_max(__builtin_elementwise_sub_sat(U2(F), st.gext), o));
+  }
+  __device__ static uint32_t Max3(uint32_t a, uint32_t b, uint32_t c) {
+    return W(__builtin_elementwise_max(__builtin_elementwise_max(U2(a), U2(b)), U2(c)));
+  }
+  __device__ static short Encode(int v) { return (short)v; }
+  __device__ static int Decode(uint32_t bits16) { return (int)bits16; }
+};
+template <> struct Cells<true> {
+  uint32_t nopen, next;  // negated penalties (f16) in both halves
+  static constexpr uint32_t kBig = 0xF753F753u;  // f16 -30000 in both halves
+  static constexpr uint32_t kOne = 0x3C003C00u;  // f16 1.0 in both halves
+  struct Step {
+    hf2 nopen, next, m;
+  };
+  __device__ static uint32_t Pair(int v) {
+    const uint32_t b = __builtin_bit_cast(unsigned short, (_Float16)v);
+    return b | (b << 16);
+  }
+  __device__ Cells(int open, int ext) : nopen(Pair(open)), next(Pair(ext)) {}
+  __device__ Step At(uint32_t end, uint32_t prev_end) const {
+    return Step{HF((nopen & ~end) | (kBig & end)), HF((next & ~end) | (kBig & end)), HF(kOne & ~prev_end)};
+  }
+  __device__ static uint32_t Diag(uint32_t h, hf2 m, uint32_t p) {
+    return W(__builtin_elementwise_fma(HF(h), m, HF(p)));
+  }
+  __device__ static void Row(const Step &st, uint32_t s, uint32_t &H, uint32_t &E, uint32_t &F) {
+    const hf2 zero = {(_Float16)0, (_Float16)0};
+    const hf2 h = __builtin_elementwise_maximum(__builtin_elementwise_maximum(HF(s), HF(E)), HF(F));
+    H = W(h);
+    const hf2 o = h + st.nopen;
+    E = W(__builtin_elementwise_maximum(__builtin_elementwise_maximum(HF(E) + st.next, o), zero));
+    F = W(__builtin_elementwise_maximum(__builtin_elementwise_maximum(HF(F) + st.next, o), zero));
+  }
+  __device__ static uint32_t Max3(uint32_t a, uint32_t b, uint32_t c) {
+    return W(__builtin_elementwise_maximum(__builtin_elementwise_maximum(HF(a), HF(b)), HF(c)));
+  }
+  __device__ static short Encode(int v) { return __builtin_bit_cast(short, (_Float16)v); }
+  __device__ static int Decode(uint32_t bits16) {
+    return (int)(float)__builtin_bit_cast(_Float16, (unsigned short)bits16);
+  }
+};
+
+template <int S, bool HALF>
 __global__ __launch_bounds__(kScoreBlock) void k_score16(ScoreArgs a) {
+  using C = Cells<HALF>;
   extern __shared__ __attribute__((aligned(16))) short s_prof16[];
   const ScoreTask t = a.tasks[blockIdx.x];
-  const uint32_t RS = a.Lpad + 8;  // int16 elements; 16-byte pad spreads LDS banks
+  const uint32_t RS = a.Lpad + 8;  // 16-bit elements; 16-byte pad spreads LDS banks
 
   const uint32_t per_slot = kProfRows * a.Lpad;
   const uint32_t total = t.q_count * per_slot;
   for (uint32_t e = threadIdx.x; e < total; e += kScoreBlock) {
     const uint32_t slot = e / per_slot, rem = e - slot * per_slot;
     const uint32_t c = rem / a.Lpad, r = rem - c * a.Lpad;
-    short v = kNeg16;
-    if (r >= a.pad)
-      v = c < 25 ? (short)a.mat[c * 32 + a.qseq[(size_t)(t.q_first + slot) * a.L + (r - a.pad)]] : (short)0;
-    s_prof16[(slot * kProfRows + c) * RS + r] = v;
+    int v = kNeg16;
+    if (r >= a.pad) v = c < 25 ? a.mat[c * 32 + a.qseq[(size_t)(t.q_first + slot) * a.L + (r - a.pad)]] : 0;
+    s_prof16[(slot * kProfRows + c) * RS + r] = C::Encode(v);
   }
   __syncthreads();
 
@@ -526,15 +605,16 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16(ScoreArgs a) {
   }
   const short *profA = s_prof16 + slotA * kProfRows * RS + i * S;
   const short *profB = s_prof16 + slotB * kProfRows * RS + i * S;
-  const us2 gopen = U2((uint32_t)(-a.open) * 0x10001u);
-  const us2 gext = U2((uint32_t)(-a.ext) * 0x10001u);
+  const C cell(a.open, a.ext);
 
   uint32_t H[S], E[S];
 #pragma unroll
   for (int k = 0; k < S; ++k) { H[k] = 0; E[k] = 0; }
-  int bestA = 0, bestB = 0, colA = 0, colB = 0;
+  uint32_t bestA = 0, bestB = 0;
+  int colA = 0, colB = 0;
   uint32_t ncols = 0;
   uint32_t hout = 0, fout = 0, hprev = 0;
+  uint32_t prev_end = 0xFFFFFFFFu;  // the column before the first one: nothing to carry
   int j = -(int)i;
   uint32_t nA = kSeqEnd, nB = kSeqEnd;
   if (j >= 0 && (uint32_t)j < wA) nA = a.db[offA + j];
@@ -550,8 +630,11 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16(ScoreArgs a) {
     nB = kSeqEnd;
     if (j + 1 >= 0 && (uint32_t)(j + 1) < wA) nA = a.db[offA + j + 1];
     if (j + 1 >= 0 && (uint32_t)(j + 1) < wB) nB = a.db[offB + j + 1];
-    // inactive columns (fill, drain, beyond the window) behave as END: state reset
+    // inactive columns (fill, drain, beyond the window) behave as END
     const bool endA = rA == kSeqEnd, endB = rB == kSeqEnd;
+    const uint32_t end = (endA ? 0x0000FFFFu : 0u) | (endB ? 0xFFFF0000u : 0u);
+    const typename C::Step st = cell.At(end, prev_end);
+    prev_end = end;
     const short *pA = profA + (rA < 25 ? rA : 25u) * RS;
     const short *pB = profB + (rB < 25 ? rB : 25u) * RS;
     uint32_t diag = diag0, F = fin, cm = 0;
@@ -562,44 +645,25 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16(ScoreArgs a) {
       const uint32_t wa[4] = {qa.x, qa.y, qa.z, qa.w}, wb[4] = {qb.x, qb.y, qb.z, qb.w};
       // diagonal sums of the chunk first, from the previous column's H, so the
       // row updates below overwrite H in place (no register rotation copies)
-      sh2 s[8];
+      uint32_t s[8];
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const uint32_t lo = __builtin_amdgcn_perm(wb[m], wa[m], 0x05040100u);
         const uint32_t hi = __builtin_amdgcn_perm(wb[m], wa[m], 0x07060302u);
-        s[2 * m] = S2(2 * m == 0 ? diag : H[k + 2 * m - 1]) + S2(lo);
-        s[2 * m + 1] = S2(H[k + 2 * m]) + S2(hi);
+        s[2 * m] = C::Diag(2 * m == 0 ? diag : H[k + 2 * m - 1], st.m, lo);
+        s[2 * m + 1] = C::Diag(H[k + 2 * m], st.m, hi);
       }
       diag = H[k + 7];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int r = k + u;
-        const sh2 h = __builtin_elementwise_max(__builtin_elementwise_max(s[u], S2(E[r])), S2(F));
-        H[r] = W(h);
-        const us2 o = __builtin_elementwise_sub_sat(U2(W(h)), gopen);
-        E[r] = W(__builtin_elementwise_max(__builtin_elementwise_sub_sat(U2(E[r]), gext), o));
-        F = W(__builtin_elementwise_max(__builtin_elementwise_sub_sat(U2(F), gext), o));
-      }
-      // column max of the chunk as a tree (a serial max chain stalls on
+      for (int u = 0; u < 8; ++u) C::Row(st, s[u], H[k + u], E[k + u], F);
+      // column max of the chunk as a tree (a serial chain stalls on
       // back-to-back dependent packed ops)
-      const us2 m01 = __builtin_elementwise_max(U2(H[k]), U2(H[k + 1]));
-      const us2 m23 = __builtin_elementwise_max(U2(H[k + 2]), U2(H[k + 3]));
-      const us2 m45 = __builtin_elementwise_max(U2(H[k + 4]), U2(H[k + 5]));
-      const us2 m67 = __builtin_elementwise_max(U2(H[k + 6]), U2(H[k + 7]));
-      const us2 m = __builtin_elementwise_max(__builtin_elementwise_max(m01, m23),
-                                              __builtin_elementwise_max(m45, m67));
-      cm = W(__builtin_elementwise_max(U2(cm), m));
+      cm = C::Max3(C::Max3(H[k], H[k + 1], H[k + 2]), C::Max3(H[k + 3], H[k + 4], H[k + 5]),
+                   C::Max3(H[k + 6], H[k + 7], cm));
     }
     hout = H[S - 1];
     fout = F;
-    if (__any(endA || endB)) {
-      const uint32_t keep = (endA ? 0xFFFF0000u : 0xFFFFFFFFu) & (endB ? 0x0000FFFFu : 0xFFFFFFFFu);
-#pragma unroll
-      for (int k = 0; k < S; ++k) { H[k] &= keep; E[k] &= keep; }
-      hout &= keep;
-      fout &= keep;
-    }
-    const int cmA = (int)(cm & 0xFFFFu), cmB = (int)(cm >> 16);
+    const uint32_t cmA = cm & 0xFFFFu, cmB = cm >> 16;
     if (!endA) {
       if (cmA >= bestA) { bestA = cmA; colA = j; }
       ++ncols;
@@ -609,11 +673,11 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16(ScoreArgs a) {
       ++ncols;
     }
   }
-  int BA = bestA, CA = colA, BB = bestB, CB = colB;
+  int BA = C::Decode(bestA), CA = colA, BB = C::Decode(bestB), CB = colB;
   for (uint32_t k = 1; k < a.G; ++k) {
     const int src = (int)(g * a.G + k);
-    const int oba = __shfl(bestA, src), oca = __shfl(colA, src);
-    const int obb = __shfl(bestB, src), ocb = __shfl(colB, src);
+    const int oba = __shfl(BA, src), oca = __shfl(CA, src);
+    const int obb = __shfl(BB, src), ocb = __shfl(CB, src);
     if (oba > BA || (oba == BA && oca > CA)) { BA = oba; CA = oca; }
     if (obb > BB || (obb == BB && ocb > CB)) { BB = obb; CB = ocb; }
   }

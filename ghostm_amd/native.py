@@ -53,6 +53,8 @@ class GhostmStats(ctypes.Structure):
         ("batches", c_uint64),
         ("score_launches", c_uint64),
         ("seed_bytes", c_uint64),
+        ("score_launches_packed", c_uint64),
+        ("score_launches_half", c_uint64),
     ]
 
     def as_dict(self) -> dict:

@@ -136,6 +136,8 @@ typedef struct GhostmStats {
   uint64_t batches;
   uint64_t score_launches;
   uint64_t seed_bytes;       /* algorithmic bytes of the K1 passes */
+  uint64_t score_launches_packed; /* K2 launches that ran a packed 16-bit kernel */
+  uint64_t score_launches_half;   /* ... of which the f16 encoding */
 } GhostmStats;
 
 /* Session: parse `aln` options exactly like the reference (getopt string

@@ -178,12 +178,25 @@ def test_reference_gpu_batching_rule(dataset):
     lib.FreeGpu()
 
 
+@pytest.mark.parametrize("kind", ["int32", "int16"])
 @pytest.mark.parametrize("ds,var,opts", [("syn_small", "default", []), ("syn_short", "default", []),
                                          ("syn_small", "r64_pam250", ["-r", "64", "-M", cases.PAM250, "-y", "2"])])
-def test_int32_score_kernel_matches_golden(ds, var, opts, dataset, golden, tmp_path):
-    """The int32 K2 kernel (used when scores may not fit int16) stays covered:
-    forced with GHOSTM_K2=int32 it reproduces the same golden outputs."""
+def test_forced_score_encoding_matches_golden(kind, ds, var, opts, dataset, golden, tmp_path):
+    """Every K2 encoding stays covered: the f16 kernel runs by default when all
+    scores fit f16's exact-integer range, the int16 one above that, int32 when
+    scores may exceed int16. Forced with GHOSTM_K2 each reproduces the golden."""
     d = dataset(ds)
-    text, st = _gpu_text(d, opts, {"GHOSTM_K2": "int32"}, str(tmp_path / "g.out"))
+    text, st = _gpu_text(d, opts, {"GHOSTM_K2": kind}, str(tmp_path / "g.out"))
     (tmp_path / "g.out").write_bytes(text)
     assert cases.sha256(str(tmp_path / "g.out")) == golden["aln"][f"{ds}/{var}"]["sha256"]
+    assert st["score_launches"] > 0 and st["score_launches_half"] == 0
+    assert st["score_launches_packed"] == (st["score_launches"] if kind == "int16" else 0)
+
+
+def test_default_encoding_is_f16_when_scores_fit(dataset, golden, tmp_path):
+    d = dataset("syn_small")
+    text, st = _gpu_text(d, [], {}, str(tmp_path / "g.out"))
+    assert st["score_launches_half"] == st["score_launches"] > 0
+    text2, st2 = _gpu_text(d, ["-M", cases.PAM250, "-G", "8", "-E", "1", "-y", "2"], {},
+                            str(tmp_path / "p.out"))
+    assert st2["score_launches_half"] == 0 and st2["score_launches_packed"] == st2["score_launches"]

@@ -1,0 +1,121 @@
+"""Summarise a tools/profile.sh run into profiles/ (tracked):
+
+  profiles/<round>_kernel_stats.csv   rocprofv3 --stats of the bench command
+  profiles/<round>_pmc.json           per kernel: launches, mean duration, HBM bytes
+                                      per launch (FETCH_SIZE x 2 x 1024 on gfx950, see
+                                      MI355X_MICROARCH.md §HBM; WRITE_SIZE x 1024), SQ
+                                      issue counters and the VALU issue utilisation
+  profiles/pmc_traffic.json           the per-launch HBM bytes bench.py reports as
+                                      roofline.traffic
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import os
+import re
+import shutil
+from collections import defaultdict
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SIMDS = 256 * 4
+
+
+def short(name: str) -> str:
+    n = re.sub(r"^void\s+", "", name)
+    n = n.split("(")[0]
+    return n.replace("ghostm::kern::", "")
+
+
+def rows(pattern: str):
+    for path in glob.glob(pattern, recursive=True):
+        with open(path, newline="") as f:
+            yield from csv.DictReader(f)
+
+
+def counters(d: str) -> dict:
+    """kernel -> counter -> list of per-dispatch values; kernel -> durations (ns)."""
+    vals: dict = defaultdict(lambda: defaultdict(dict))
+    dur: dict = defaultdict(dict)
+    for r in rows(os.path.join(d, "**", "*counter_collection.csv")):
+        k = short(r["Kernel_Name"])
+        disp = r.get("Dispatch_Id") or r.get("Correlation_Id")
+        vals[k][r["Counter_Name"]][disp] = vals[k][r["Counter_Name"]].get(disp, 0.0) + float(r["Counter_Value"])
+        if r.get("Start_Timestamp") and r.get("End_Timestamp"):
+            dur[k][disp] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    return vals, dur
+
+
+def mean(xs):
+    xs = list(xs)
+    return sum(xs) / len(xs) if xs else None
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--round", required=True)
+    ap.add_argument("--prof", required=True)
+    ap.add_argument("--queries", type=int, required=True)
+    args = ap.parse_args()
+    prof = os.path.join(REPO, "profiles")
+    os.makedirs(prof, exist_ok=True)
+
+    stats = glob.glob(os.path.join(args.prof, "trace", "**", "*kernel_stats.csv"), recursive=True)
+    kernels: dict = {}
+    if stats:
+        shutil.copy(stats[0], os.path.join(prof, f"{args.round}_kernel_stats.csv"))
+        for r in rows(stats[0]):
+            kernels[short(r["Name"])] = {"launches_in_trace": int(r["Calls"]),
+                                         "avg_ms_trace": float(r["AverageNs"]) / 1e6,
+                                         "percent_of_gpu_time": float(r["Percentage"])}
+
+    fetch, _ = counters(os.path.join(args.prof, "fetch"))
+    write, _ = counters(os.path.join(args.prof, "write"))
+    sq, sq_dur = counters(os.path.join(args.prof, "sq"))
+    for k in set(fetch) | set(write) | set(sq):
+        e = kernels.setdefault(k, {})
+        f = mean(fetch.get(k, {}).get("FETCH_SIZE", {}).values())
+        w = mean(write.get(k, {}).get("WRITE_SIZE", {}).values())
+        if f is not None:
+            e["fetch_size_kb_raw"] = f
+            e["hbm_read_bytes_per_launch"] = f * 1024 * 2  # gfx950: FETCH_SIZE reads 1/2
+        if w is not None:
+            e["hbm_write_bytes_per_launch"] = w * 1024
+        if f is not None and w is not None:
+            e["hbm_bytes_per_launch"] = e["hbm_read_bytes_per_launch"] + e["hbm_write_bytes_per_launch"]
+        if k in sq:
+            c = {name: mean(v.values()) for name, v in sq[k].items()}
+            e["sq"] = c
+            d = mean(sq_dur.get(k, {}).values())
+            if d:
+                e["avg_ms_pmc_pass"] = d / 1e6
+            # a wave64 VALU instruction occupies its SIMD for 2 cycles; the clock is
+            # GRBM_GUI_ACTIVE / 8 XCDs over the dispatch (MI355X_MICROARCH.md, DVFS)
+            if c.get("SQ_INSTS_VALU") and c.get("GRBM_GUI_ACTIVE"):
+                cyc = c["GRBM_GUI_ACTIVE"] / 8
+                e["valu_issue_util"] = c["SQ_INSTS_VALU"] * 2 / (SIMDS * cyc)
+                if d:
+                    e["effective_clock_ghz"] = cyc / d
+    with open(os.path.join(prof, f"{args.round}_pmc.json"), "w") as f:
+        json.dump({"round": args.round, "queries": args.queries, "kernels": kernels}, f, indent=1, sort_keys=True)
+
+    def fam(prefix):
+        best = [k for k in kernels if k.startswith(prefix) and "hbm_bytes_per_launch" in kernels[k]]
+        if not best:
+            return None
+        k = max(best, key=lambda x: kernels[x].get("percent_of_gpu_time", 0))
+        return kernels[k]["hbm_bytes_per_launch"]
+
+    traffic = {"round": args.round, "queries": args.queries,
+               "note": "HBM bytes per launch = FETCH_SIZE*2*1024 + WRITE_SIZE*1024 (gfx950 correction)",
+               "k_score_hbm_bytes_per_launch": fam("k_score"),
+               "k_seed_hbm_bytes_per_launch": fam("k_seed<")}
+    with open(os.path.join(prof, "pmc_traffic.json"), "w") as f:
+        json.dump(traffic, f, indent=1)
+    print(json.dumps(traffic))
+
+
+if __name__ == "__main__":
+    main()
