@@ -184,9 +184,15 @@ def main() -> None:
         score_cells = per["score_cells"] / max(1, per["score_launches"])
         achieved = score_cells * SCORE_OPS_PER_CELL / score_t / 1e12 if score_t > 0 else 0.0
         packed = per["score_launches_packed"] == per["score_launches"] and per["score_launches"] > 0
+        half = packed and per["score_launches_half"] == per["score_launches"]
         peak = PEAK_VALU_PK16_TOPS if packed else PEAK_VALU_TOPS
-        kname = ("k_score16 (K2 Gotoh DP, packed int16 VALU, two candidates per lane)" if packed
-                 else "k_score (K2 Gotoh DP, int32 VALU)")
+        if half:
+            kname = "k_score16<32,f16> (K2 Gotoh DP, packed f16 holding exact integers, two candidates per lane)"
+        elif packed:
+            kname = "k_score16<32,int16> (K2 Gotoh DP, packed int16, two candidates per lane)"
+        else:
+            kname = "k_score (K2 Gotoh DP, int32)"
+        dtype = "f16" if half else ("int16" if packed else "int32")
         pmc = load_pmc_traffic()
         traffic = None
         if pmc and pmc.get("queries") == args.queries:
@@ -203,7 +209,7 @@ def main() -> None:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "int16" if packed else "int32",
+            "dtype": dtype,
             "data": "synthetic (ghostm synth, splitmix64 seed 4; BLOSUM62 11/1 defaults)",
             "config": {
                 "workload": "cfg4: synthetic 1M queries (avg 300 aa requested, L=127) x 10M-residue DB, per rank",

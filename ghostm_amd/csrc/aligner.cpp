@@ -381,13 +381,18 @@ void Session::DeviceMergePath(QueryData &q, DbData &d, const std::vector<uint32_
   const uint32_t base = q.chunk.L + 2 * opt_.extend + 2 * (1u << opt_.log_region);
   const uint32_t tb_base = q.chunk.L + 2 * opt_.extend * 2 * (1u << opt_.log_region);
   const uint32_t cap = std::max<uint32_t>(opt_.best, 1);
-  const uint64_t kSegmentCands = 8ull << 20;
+  // segments of ~8M candidates; the last one ~1M, so the formatting left after
+  // the GPU finishes is short
+  const uint64_t kSegmentCands = 8ull << 20, kTailCands = 1ull << 20;
   const uint32_t ng = (uint32_t)q.group_first.size();
   auto group_begin = [&](uint32_t g) { return offsets[q.group_first[g]]; };
   uint32_t g0 = 0;
   while (g0 < ng) {
+    const uint64_t rem = total - group_begin(g0);
+    const uint64_t target =
+        (rem > kTailCands && rem <= kSegmentCands + kTailCands) ? rem - kTailCands : kSegmentCands;
     uint32_t g1 = g0 + 1;
-    while (g1 < ng && group_begin(g1) - group_begin(g0) < kSegmentCands) ++g1;
+    while (g1 < ng && group_begin(g1) - group_begin(g0) < target) ++g1;
     const uint64_t c0 = group_begin(g0);
     const uint64_t c1 = g1 < ng ? group_begin(g1) : total;
     if (c1 > c0) {
@@ -516,32 +521,36 @@ struct LineWriter {
 };
 }  // namespace
 
+void Session::Part::Reset(size_t pieces) {
+  text.resize(pieces);
+  hits.resize(pieces);
+  for (std::string &t : text) t.clear();
+  for (std::vector<GhostmHit> &h : hits) h.clear();
+}
+
 Session::Part *Session::NewPart() {
-  parts_.emplace_back();
-  return &parts_.back();
+  if (used_parts_ == parts_.size()) parts_.emplace_back();
+  return &parts_[used_parts_++];
 }
 
 void Session::FormatResults(const QueryData &q, const Results &results, Part *out) {
   const uint32_t n = q.chunk.nseq;
-  std::vector<Part> local(threads_);
+  out->Reset(threads_);
   const LineWriter w{opt_.output_style, EvalueCalculator(opt_.karlin)};
   ParallelFor(n, threads_, [&](size_t b, size_t e, unsigned t) {
-    Part &p = local[t];
+    std::string &text = out->text[t];
+    std::vector<GhostmHit> &hits = out->hits[t];
     for (size_t i = b; i < e; ++i) {
       const uint64_t space = (uint64_t)q.qlen[i] * (uint64_t)db_sum_u32_;
       for (const HitRecord &h : results[i]) {
         const DbData &d = dbs_[h.db_chunk];
-        w.Write(&p.text, q.chunk.names[i], d.chunk.names[h.subject], h.score, h.start, h.end, h.aln_len,
+        w.Write(&text, q.chunk.names[i], d.chunk.names[h.subject], h.score, h.start, h.end, h.aln_len,
                 h.aln_match, h.seq_id, space);
-        p.hits.push_back(GhostmHit{q.global_base + (uint32_t)i, d.global_base + h.subject, h.score, h.start,
-                                   h.end, h.aln_len, h.aln_match, h.seq_id});
+        hits.push_back(GhostmHit{q.global_base + (uint32_t)i, d.global_base + h.subject, h.score, h.start,
+                                 h.end, h.aln_len, h.aln_match, h.seq_id});
       }
     }
   });
-  for (Part &p : local) {
-    out->text.append(p.text);
-    out->hits.insert(out->hits.end(), p.hits.begin(), p.hits.end());
-  }
 }
 
 // Same text from the device-selected hits: a name group's lines are printed
@@ -550,12 +559,16 @@ void Session::FormatSelected(const QueryData &q, uint32_t g0, const std::vector<
                              const std::vector<SelectedHit> &hits, uint32_t cap, Part *out) {
   const uint32_t ng = (uint32_t)counts.size();
   const unsigned workers = std::max(1u, threads_ > 1 ? threads_ - 1 : 1u);
-  std::vector<Part> local(workers);
+  out->Reset(workers);
   const LineWriter w{opt_.output_style, EvalueCalculator(opt_.karlin)};
   const DbData &d = dbs_[0];
   ParallelFor(ng, workers, [&](size_t b, size_t e, unsigned t) {
-    Part &p = local[t];
-    p.text.reserve((e - b) * cap * 64);
+    std::string &text = out->text[t];
+    std::vector<GhostmHit> &ph = out->hits[t];
+    size_t nh = 0;
+    for (size_t g = b; g < e; ++g) nh += counts[g];
+    text.reserve(nh * 96);
+    ph.reserve(nh);
     for (size_t g = b; g < e; ++g) {
       const uint32_t i = q.group_last[g0 + g];
       const std::string &name = q.chunk.names[i];
@@ -564,20 +577,12 @@ void Session::FormatSelected(const QueryData &q, uint32_t g0, const std::vector<
         const SelectedHit &h = hits[(size_t)g * cap + k];
         const uint32_t len = h.ml >> 8, match = h.ml & 0xFFu;
         const float seq_id = (float)match / (float)len;  // aligner.cpp:945
-        w.Write(&p.text, name, d.chunk.names[h.sid], h.score, h.start, h.end, len, match, seq_id, space);
-        p.hits.push_back(GhostmHit{q.global_base + i, d.global_base + h.sid, h.score, h.start, h.end, len,
-                                   match, seq_id});
+        w.Write(&text, name, d.chunk.names[h.sid], h.score, h.start, h.end, len, match, seq_id, space);
+        ph.push_back(GhostmHit{q.global_base + i, d.global_base + h.sid, h.score, h.start, h.end, len, match,
+                               seq_id});
       }
     }
   });
-  size_t bytes = 0, nh = 0;
-  for (Part &p : local) { bytes += p.text.size(); nh += p.hits.size(); }
-  out->text.reserve(bytes);
-  out->hits.reserve(nh);
-  for (Part &p : local) {
-    out->text.append(p.text);
-    out->hits.insert(out->hits.end(), p.hits.begin(), p.hits.end());
-  }
 }
 
 void Session::Run() {
@@ -586,7 +591,7 @@ void Session::Run() {
   dev.ResetTimes();
   stats_ = GhostmStats{};
   merge_epoch_ = 0;
-  parts_.clear();
+  used_parts_ = 0;
   joined_.clear();
   joined_valid_ = false;
   hits_.clear();
@@ -609,16 +614,19 @@ void Session::Run() {
   stats_.seed_bytes = dt.seed_bytes;
   stats_.score_cells = dt.score_cells;
   stats_.traceback_cells = dt.traceback_cells;
-  for (const Part &p : parts_) stats_.hits += p.hits.size();
+  for (size_t k = 0; k < used_parts_; ++k)
+    for (const auto &h : parts_[k].hits) stats_.hits += h.size();
 }
 
 const std::string &Session::Output() {
   if (!joined_valid_) {
     size_t n = 0;
-    for (const Part &p : parts_) n += p.text.size();
+    for (size_t k = 0; k < used_parts_; ++k)
+      for (const std::string &t : parts_[k].text) n += t.size();
     joined_.clear();
     joined_.reserve(n);
-    for (const Part &p : parts_) joined_.append(p.text);
+    for (size_t k = 0; k < used_parts_; ++k)
+      for (const std::string &t : parts_[k].text) joined_.append(t);
     joined_valid_ = true;
   }
   return joined_;
@@ -627,7 +635,8 @@ const std::string &Session::Output() {
 const std::vector<GhostmHit> &Session::Hits() {
   if (!hits_valid_) {
     hits_.clear();
-    for (const Part &p : parts_) hits_.insert(hits_.end(), p.hits.begin(), p.hits.end());
+    for (size_t k = 0; k < used_parts_; ++k)
+      for (const auto &h : parts_[k].hits) hits_.insert(hits_.end(), h.begin(), h.end());
     hits_valid_ = true;
   }
   return hits_;
@@ -635,7 +644,8 @@ const std::vector<GhostmHit> &Session::Hits() {
 
 void Session::WriteOutputFile() {
   std::ofstream out(opt_.output_file.c_str(), std::ios::binary);
-  for (const Part &p : parts_) out.write(p.text.data(), (std::streamsize)p.text.size());
+  for (size_t k = 0; k < used_parts_; ++k)
+    for (const std::string &t : parts_[k].text) out.write(t.data(), (std::streamsize)t.size());
 }
 
 }  // namespace ghostm
