@@ -110,7 +110,7 @@ def main() -> None:
 
         torch.cuda.set_device(_device())
         dist.init_process_group("nccl")
-    from ghostm_amd.aligner import HIT_DTYPE, Session
+    from ghostm_amd.aligner import Session
 
     workdir = args.workdir or tempfile.mkdtemp(prefix=f"ghostm_bench_r{rank}_")
     t0 = time.perf_counter()
@@ -122,21 +122,10 @@ def main() -> None:
     def step():
         sess.run()
         if dist is not None:
-            import numpy as np
-            import torch
+            from ghostm_amd.shard import gather_hits
 
-            hits = sess.hits()
-            payload = torch.from_numpy(hits.view(np.uint8)).cuda()
-            n = torch.tensor([payload.numel()], device="cuda", dtype=torch.int64)
-            sizes = [torch.zeros_like(n) for _ in range(world)]
-            dist.all_gather(sizes, n)
-            cap = int(max(int(s.item()) for s in sizes))
-            buf = torch.zeros(cap, dtype=torch.uint8, device="cuda")
-            buf[: payload.numel()] = payload
-            gathered = [torch.zeros_like(buf) for _ in range(world)] if rank == 0 else None
-            dist.gather(buf, gathered, dst=0)
+            merged = gather_hits(sess.hits(), dist, "cuda")
             if rank == 0:
-                merged = [g[: int(s.item())].cpu().numpy().view(HIT_DTYPE) for g, s in zip(gathered, sizes)]
                 step.gathered = sum(len(m) for m in merged)
     step.gathered = 0
 

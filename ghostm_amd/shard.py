@@ -1,0 +1,67 @@
+"""Query sharding and the single hit-record gather of the multi-GPU path
+(SURVEY.md §8 e1).
+
+One process per GPU: rank r searches its own contiguous query range against a
+full DB replica; nothing crosses ranks on the data path. At the end the 32-byte
+hit records (`GhostmHit`, include/ghostm_hip.h) of every rank are gathered to
+rank 0 in rank order — with contiguous shards that is the single-GPU output
+order. Over RCCL (backend "nccl") on GPUs; the same code runs over gloo on CPU
+for the tests.
+"""
+from __future__ import annotations
+
+from typing import Sequence
+
+import numpy as np
+
+
+def balanced_cuts(weights: Sequence[int], names: Sequence[str], world: int) -> list[int]:
+    """Cut points c[0]=0 <= ... <= c[world]=n splitting queries into `world`
+    contiguous shards of about equal total weight (e.g. residues), never inside a
+    group of consecutive equal names — the reference merges such a group (DNA
+    frames) into one result list (aligner.cpp:697-700), so it must stay on one rank."""
+    n = len(weights)
+    if len(names) != n:
+        raise ValueError("weights and names differ in length")
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    # group starts: a query starts a group unless its name equals the previous one
+    starts = [i for i in range(n) if i == 0 or names[i] != names[i - 1]]
+    prefix = np.concatenate([[0], np.cumsum(np.asarray(weights, dtype=np.int64))])
+    total = int(prefix[-1])
+    cuts = [0]
+    for r in range(1, world):
+        target = total * r / world
+        # first group start whose prefix weight reaches the target
+        best = n
+        for s in starts:
+            if s >= cuts[-1] and prefix[s] >= target:
+                best = s
+                break
+        cuts.append(max(cuts[-1], best))
+    cuts.append(n)
+    return cuts
+
+
+def gather_hits(hits: np.ndarray, dist, device) -> list[np.ndarray] | None:
+    """Gather every rank's hit records (a structured array of any dtype) to rank 0.
+    Returns the per-rank arrays in rank order on rank 0, None elsewhere. Sizes
+    differ per rank, so an all_gather of the byte counts precedes one gather of
+    buffers padded to the largest."""
+    import torch
+
+    world = dist.get_world_size()
+    rank = dist.get_rank()
+    raw = np.ascontiguousarray(hits).view(np.uint8).reshape(-1)
+    payload = torch.from_numpy(raw.copy()).to(device)
+    n = torch.tensor([payload.numel()], device=device, dtype=torch.int64)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n)
+    cap = max(int(s.item()) for s in sizes)
+    buf = torch.zeros(max(cap, 1), dtype=torch.uint8, device=device)
+    buf[: payload.numel()] = payload
+    gathered = [torch.zeros_like(buf) for _ in range(world)] if rank == 0 else None
+    dist.gather(buf, gathered, dst=0)
+    if rank != 0:
+        return None
+    return [g[: int(s.item())].cpu().numpy().view(hits.dtype) for g, s in zip(gathered, sizes)]

@@ -200,3 +200,22 @@ def test_default_encoding_is_f16_when_scores_fit(dataset, golden, tmp_path):
     text2, st2 = _gpu_text(d, ["-M", cases.PAM250, "-G", "8", "-E", "1", "-y", "2"], {},
                             str(tmp_path / "p.out"))
     assert st2["score_launches_half"] == 0 and st2["score_launches_packed"] == st2["score_launches"]
+
+
+REF_GPU_VARIANTS = [v for v in cases.VARIANTS
+                    if f"{v[0]}/{v[1]}" in ("protein_testset/y0", "readme_kat/default", "syn_small/default",
+                                            "syn_small/r64_pam250", "syn_dna/default", "syn_chunks/default",
+                                            "syn_short/default")]
+
+
+@pytest.mark.skipif(not os.path.exists(cases.REF), reason="reference build (oracle/_ref) absent")
+@pytest.mark.parametrize("ds,var,opts,env", REF_GPU_VARIANTS, ids=[f"{v[0]}/{v[1]}" for v in REF_GPU_VARIANTS])
+def test_reference_driver_on_this_plugin(ds, var, opts, env, dataset, golden, tmp_path):
+    """The drop-in itself: the reference's own aligner.cpp (oracle/_ref, compiled from
+    the reference sources and linked against libghostm_hip.so) run with -D 0 drives
+    this repo's HIP kernels through the reference plugin ABI (InitGpu ... SearchNextGpu,
+    CalculateScoreGpu ... FreeGpu) and must print the reference CPU path's bytes."""
+    d = dataset(ds)
+    out = str(tmp_path / "ref_gpu.out")
+    cases.run_aln(cases.REF, d, list(opts) + ["-D", "0"], env, out)
+    assert cases.sha256(out) == golden["aln"][f"{ds}/{var}"]["sha256"]
