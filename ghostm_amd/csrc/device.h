@@ -16,6 +16,10 @@
 
 namespace ghostm {
 
+namespace kern {
+struct TbArgs;
+}
+
 struct SeedConfig {
   uint32_t seed_mask = 15;   // index seed bits (db -k 4 -> 0b1111)
   uint32_t threshold = 2;    // aln -t
@@ -45,6 +49,7 @@ struct DeviceTimes {
   uint64_t seed_bytes = 0;
   uint64_t score_launches = 0, score_launches_packed = 0, score_launches_half = 0;
   uint64_t score_cells = 0, traceback_cells = 0;
+  uint64_t traceback_launches = 0, traceback_launches_key = 0;
 };
 
 class DeviceModule {
@@ -103,6 +108,7 @@ class DeviceModule {
 
  private:
   DeviceModule() = default;
+  void LaunchTraceback(kern::TbArgs a, uint32_t rows, uint32_t n);
   int device_ = -1;
   void *stream_ = nullptr;
   DeviceTimes times_;

@@ -91,7 +91,7 @@ struct DevDb {
 
 struct DeviceModule::Impl {
   int h_matrix[32 * 32] = {0};
-  DevBuf mat_k2, mat_tb;
+  DevBuf mat_k2, mat_tb, mat_tbk;
   // K1 work
   DevBuf counts, nelem, slots, offsets, qlist, gbuf, gbuf_off, list_beg, list_len;
   DevBuf cand_start, cand_qid;
@@ -161,10 +161,21 @@ void DeviceModule::SetMatrix(const int *m) {
                                                 : (int)(((unsigned)v << 16) | (unsigned)inc);
     }
   }
+  // K3 key table: (score << 18) | (2 << 16) | (0x80 | eq); padding rows score far
+  // below any reachable h (k_traceback_key)
+  int tbk[32 * 32];
+  for (int c = 0; c < 32; ++c) {
+    for (int q = 0; q < 32; ++q) {
+      const int v = q == (int)kern::kPadCode ? -4096 : std::max(-4096, std::min(4095, m[c * 32 + q]));
+      tbk[c * 32 + q] = (int)(((uint32_t)v << 18) | (2u << 16) | 0x80u | (c == q ? 1u : 0u));
+    }
+  }
   impl_->mat_k2.Reserve(sizeof(k2));
   impl_->mat_tb.Reserve(sizeof(tb));
+  impl_->mat_tbk.Reserve(sizeof(tbk));
   HIP_CHECK(hipMemcpy(impl_->mat_k2.p, k2, sizeof(k2), hipMemcpyHostToDevice));
   HIP_CHECK(hipMemcpy(impl_->mat_tb.p, tb, sizeof(tb), hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(impl_->mat_tbk.p, tbk, sizeof(tbk), hipMemcpyHostToDevice));
   impl_->matrix_set = true;
 }
 
@@ -547,6 +558,42 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
   times_.score_cells += cells;
 }
 
+// K3 launch: the key formulation when its field widths hold (len < 511,
+// matches < 128, |h| < 8192), else the int32 kernel. GHOSTM_K3=int32 forces it.
+void DeviceModule::LaunchTraceback(kern::TbArgs a, uint32_t rows, uint32_t n) {
+  Impl &I = *impl_;
+  const Layout lay = ChooseLayout(rows, a.base);
+  a.Lpad = lay.Lpad;
+  a.G = lay.G;
+  a.gpw = lay.gpw;
+  int max_abs = 0;
+  for (int v : I.h_matrix) max_abs = std::max(max_abs, v < 0 ? -v : v);
+  const char *force = getenv("GHOSTM_K3");
+  const bool key = !(force && strcmp(force, "int32") == 0) && a.L <= 127 && lay.Lpad + a.base < 500 &&
+                   (int64_t)a.L * max_abs < 4000 && a.open <= 0 && a.ext <= 0 && -a.open < 4000 &&
+                   -a.ext < 4000;
+  if (key) a.mat_tb = I.mat_tbk.as<int>();
+  const uint32_t per_block = (kern::kTbBlock / 64) * lay.gpw;
+  const dim3 grid((n + per_block - 1) / per_block), block(kern::kTbBlock);
+  switch (lay.S) {
+    case 32:
+      if (key) hipLaunchKernelGGL(kern::k_traceback_key<32>, grid, block, 0, S(stream_), a);
+      else hipLaunchKernelGGL(kern::k_traceback<32>, grid, block, 0, S(stream_), a);
+      break;
+    case 16:
+      if (key) hipLaunchKernelGGL(kern::k_traceback_key<16>, grid, block, 0, S(stream_), a);
+      else hipLaunchKernelGGL(kern::k_traceback<16>, grid, block, 0, S(stream_), a);
+      break;
+    default:
+      if (key) hipLaunchKernelGGL(kern::k_traceback_key<8>, grid, block, 0, S(stream_), a);
+      else hipLaunchKernelGGL(kern::k_traceback<8>, grid, block, 0, S(stream_), a);
+      break;
+  }
+  HIP_CHECK(hipGetLastError());
+  times_.traceback_launches += 1;
+  times_.traceback_launches_key += key ? 1 : 0;
+}
+
 void DeviceModule::MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, uint64_t cand_begin, uint64_t n,
                                uint32_t best, uint32_t tb_base, int open, int ext,
                                std::vector<uint32_t> *counts, std::vector<SelectedHit> *hits) {
@@ -596,13 +643,9 @@ void DeviceModule::MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, 
   times_.merge += ElapsedMs(I.ev0, I.ev1) * 1e-3;
 
   // K3 over the slots (empty slots carry qid 0xFFFFFFFF and are skipped)
-  const Layout lay = ChooseLayout(q->L, tb_base);
   kern::TbArgs a{};
   a.qseq = q->seq.as<uint8_t>();
   a.L = q->L;
-  a.Lpad = lay.Lpad;
-  a.G = lay.G;
-  a.gpw = lay.gpw;
   a.db = d->seq.as<uint8_t>();
   a.mat_tb = I.mat_tb.as<int>();
   a.qid = I.tb_qid.as<uint32_t>();
@@ -616,15 +659,8 @@ void DeviceModule::MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, 
   I.counters.Reserve(16);
   HIP_CHECK(hipMemsetAsync(I.counters.p, 0, 16, S(stream_)));
   a.cells = I.counters.as<unsigned long long>() + 1;
-  const uint32_t per_block = (kern::kTbBlock / 64) * lay.gpw;
-  const dim3 grid((uint32_t)((slots + per_block - 1) / per_block)), block(kern::kTbBlock);
   HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
-  switch (lay.S) {
-    case 32: hipLaunchKernelGGL(kern::k_traceback<32>, grid, block, 0, S(stream_), a); break;
-    case 16: hipLaunchKernelGGL(kern::k_traceback<16>, grid, block, 0, S(stream_), a); break;
-    default: hipLaunchKernelGGL(kern::k_traceback<8>, grid, block, 0, S(stream_), a); break;
-  }
-  HIP_CHECK(hipGetLastError());
+  LaunchTraceback(a, q->L, (uint32_t)slots);
   HIP_CHECK(hipEventRecord(I.ev1, S(stream_)));
   hipLaunchKernelGGL(kern::k_finalize, dim3((uint32_t)((slots + 255) / 256)), dim3(256), 0, S(stream_),
                      I.sel_count.as<uint32_t>(), I.sel_cand.as<uint32_t>(), I.sel_sid.as<uint32_t>(),
@@ -650,7 +686,6 @@ void DeviceModule::TraceBack(DevQuery *q, DevDb *d, uint32_t n, const uint32_t *
                              float *seq_id) {
   Impl &I = *impl_;
   if (n == 0) return;
-  const Layout lay = ChooseLayout(q->L, base);
   I.tb_qid.Reserve((size_t)n * 4);
   I.tb_end.Reserve((size_t)n * 4);
   I.tb_start.Reserve((size_t)n * 4);
@@ -660,9 +695,6 @@ void DeviceModule::TraceBack(DevQuery *q, DevDb *d, uint32_t n, const uint32_t *
   kern::TbArgs a{};
   a.qseq = q->seq.as<uint8_t>();
   a.L = q->L;
-  a.Lpad = lay.Lpad;
-  a.G = lay.G;
-  a.gpw = lay.gpw;
   a.db = d->seq.as<uint8_t>();
   a.mat_tb = I.mat_tb.as<int>();
   a.qid = I.tb_qid.as<uint32_t>();
@@ -676,15 +708,8 @@ void DeviceModule::TraceBack(DevQuery *q, DevDb *d, uint32_t n, const uint32_t *
   I.counters.Reserve(16);
   HIP_CHECK(hipMemsetAsync(I.counters.p, 0, 16, S(stream_)));
   a.cells = I.counters.as<unsigned long long>() + 1;
-  const uint32_t per_block = (kern::kTbBlock / 64) * lay.gpw;
-  const dim3 grid((n + per_block - 1) / per_block), block(kern::kTbBlock);
   HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
-  switch (lay.S) {
-    case 32: hipLaunchKernelGGL(kern::k_traceback<32>, grid, block, 0, S(stream_), a); break;
-    case 16: hipLaunchKernelGGL(kern::k_traceback<16>, grid, block, 0, S(stream_), a); break;
-    default: hipLaunchKernelGGL(kern::k_traceback<8>, grid, block, 0, S(stream_), a); break;
-  }
-  HIP_CHECK(hipGetLastError());
+  LaunchTraceback(a, q->L, n);
   HIP_CHECK(hipEventRecord(I.ev1, S(stream_)));
   std::vector<uint32_t> ml(n);
   HIP_CHECK(hipMemcpyAsync(db_start, I.tb_start.p, (size_t)n * 4, hipMemcpyDeviceToHost, S(stream_)));

@@ -764,23 +764,38 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback(TbArgs a) {
       const int *row = s_mat + c * 32;
       int diag = diag0, tml = tml0, F = fin, hup = hin, mup = min_;
 #pragma unroll
-      for (int u = 0; u < S; ++u) {
-        const int P = row[(qcode[u >> 2] >> (8 * (u & 3))) & 0xFFu];
-        const int s = diag + (P >> 16);
-        int h = 0, ml = 0;
-        if (s > 0) { h = s; ml = tml + (P & 0xFFFF); }
-        const int e = max(E[u] + ext, H[u] + open);
-        E[u] = e;
-        if (e > h) { h = e; ml = M[u] + 0x100; }
-        F = max(F + ext, hup + open);
-        if (F > h) { h = F; ml = mup + 0x100; }
-        diag = H[u];
-        tml = M[u];
-        H[u] = h;
-        M[u] = ml;
-        hup = h;
-        mup = ml;
-        if (h > best) { best = h; best_col = j; best_ml = ml; }
+      for (int k = 0; k < S; k += 4) {
+        // diagonal terms of the chunk from the previous column's H/M first, so
+        // the row updates overwrite H/M in place (no register rotation copies)
+        int sd[4], md[4];
+        const uint32_t qw = qcode[k >> 2];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int P = row[(qw >> (8 * v)) & 0xFFu];
+          const int dh = v == 0 ? diag : H[k + v - 1];
+          const int dm = v == 0 ? tml : M[k + v - 1];
+          sd[v] = dh + (P >> 16);
+          md[v] = dm + (P & 0xFFFF);
+        }
+        diag = H[k + 3];
+        tml = M[k + 3];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int u = k + v;
+          const int s = sd[v];
+          int h = 0, ml = 0;
+          if (s > 0) { h = s; ml = md[v]; }
+          const int e = max(E[u] + ext, H[u] + open);
+          E[u] = e;
+          if (e > h) { h = e; ml = M[u] + 0x100; }
+          F = max(F + ext, hup + open);
+          if (F > h) { h = F; ml = mup + 0x100; }
+          H[u] = h;
+          M[u] = ml;
+          hup = h;
+          mup = ml;
+          if (h > best) { best = h; best_col = j; best_ml = ml; }
+        }
       }
       hout = H[S - 1];
       fout = F;
@@ -800,6 +815,122 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback(TbArgs a) {
   if (valid && i == 0) {
     a.out_start[hit] = p0 - (uint32_t)C;
     a.out_ml[hit] = (uint32_t)ML;
+  }
+  WaveAddCells(a.cells, (valid && i == 0) ? (unsigned long long)ncols * a.L : 0ull);
+}
+
+// k_traceback_key: the same reverse DP with each cell's (h, ml) folded into one
+// 32-bit key  h << 18 | prio << 16 | ml  (ml = len << 7 | matches). The
+// reference's selection — h = s if s > 0 else 0, then E if e > h, then F if
+// F > h, each strict — is a plain max over keys whose priorities order the
+// ties: zero (3) > diagonal (2) > E (1) > F (0). The E and F chains carry only
+// their score; their ml comes from the left / upper cell (the reference's
+// quirk), spliced in with one v_bfi. Per cell: table lookup, ~14 integer ops
+// and the strict first-maximum update. Used when len < 511, L <= 127 and every
+// |h| < 8192; k_traceback above covers the rest.
+constexpr uint32_t kKeyLow = (1u << 18) - 1;  // prio + ml bits
+constexpr uint32_t kKeyPrio = 3u << 16;
+
+__device__ inline int ShiftUpI(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xF, 0xF, false); }
+
+template <int S>
+__global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
+  __shared__ int s_key[32 * 32];
+  for (uint32_t e = threadIdx.x; e < 32 * 32; e += kTbBlock) s_key[e] = a.mat_tb[e];
+  __syncthreads();
+
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t g = lane / a.G, i = lane - g * a.G;
+  const uint32_t hit = (blockIdx.x * (kTbBlock / 64) + wave) * a.gpw + g;
+  const bool valid = g < a.gpw && hit < a.n && a.qid[hit] != 0xFFFFFFFFu;
+  uint32_t p0 = 0, width = 0;
+  // byte offset of processing row U = i*S + u's query code inside a table row;
+  // row U walks the query backwards: position Lpad-1-U
+  uint32_t qoff[S];
+#pragma unroll
+  for (int u = 0; u < S; ++u) qoff[u] = kPadCode * 4;
+  if (valid) {
+    p0 = a.end[hit];
+    width = p0 < a.base ? p0 + 1 : a.base;
+    const uint8_t *qs = a.qseq + (size_t)a.qid[hit] * a.L;
+#pragma unroll
+    for (int u = 0; u < S; ++u) {
+      const int k = (int)a.Lpad - 1 - (int)(i * S + u);
+      if (k >= 0 && k < (int)a.L) qoff[u] = (uint32_t)qs[k] * 4;
+    }
+  }
+  int K[S], KE[S];
+#pragma unroll
+  for (int u = 0; u < S; ++u) { K[u] = 0; KE[u] = 0; }
+  int bestK = 0, bestX = (int)kKeyLow, best_col = 0;
+  int kout = 0, kfout = 0, kprev = 0;
+  bool done = false;
+  uint32_t ncols = 0;
+  const int OPENK = (int)(((uint32_t)a.open << 18) | (1u << 16) | 0x80u);  // E: prio 1, len + 1
+  const int OPENKF = (int)(((uint32_t)a.open << 18) | 0x80u);              // F: prio 0, len + 1
+  const int EXTK = (int)((uint32_t)a.ext << 18);
+  const int KZ = (int)(3u << 16);
+  const uint32_t HIGH = ~kKeyLow;
+  int j = -(int)i;
+  const uint32_t steps = a.base + a.G - 1;
+  for (uint32_t step = 0; step < steps; ++step, ++j) {
+    int kin = ShiftUpI(kout), kfin = ShiftUpI(kfout);
+    if (i == 0) { kin = 0; kfin = 0; }
+    const int kdiag0 = kprev;
+    kprev = kin;
+    bool active = valid && !done && j >= 0 && (uint32_t)j < width;
+    uint32_t c = 0;
+    if (active) {
+      c = a.db[p0 - j];
+      if (c == kSeqEnd) { done = true; active = false; }
+    }
+    if (active) {
+      const char *rowp = reinterpret_cast<const char *>(s_key) + c * 128;
+      int kd = kdiag0, KF = kfin, kup = kin;
+#pragma unroll
+      for (int k = 0; k < S; k += 4) {
+        // diagonal keys of the chunk from the previous column first, so the rows
+        // below overwrite K in place
+        int ks[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          ks[v] = (v == 0 ? kd : K[k + v - 1]) + *reinterpret_cast<const int *>(rowp + qoff[k + v]);
+        kd = K[k + 3];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int u = k + v;
+          const int k1 = max(ks[v], KZ);
+          const int A = K[u] + OPENK;
+          const int B = (int)((((uint32_t)(KE[u] + EXTK)) & HIGH) | ((uint32_t)A & kKeyLow));
+          KE[u] = max(A, B);
+          const int AF = kup + OPENKF;
+          const int BF = (int)((((uint32_t)(KF + EXTK)) & HIGH) | ((uint32_t)AF & kKeyLow));
+          KF = max(AF, BF);
+          const int kc = (int)((uint32_t)max(max(k1, KE[u]), KF) & ~kKeyPrio);
+          K[u] = kc;
+          kup = kc;
+          if (kc > bestX) { bestK = kc; bestX = kc | (int)kKeyLow; best_col = j; }
+        }
+      }
+      kout = K[S - 1];
+      kfout = KF;
+      ++ncols;
+    } else {
+      kout = 0;
+      kfout = 0;
+    }
+  }
+  // first cell (column-major, rows in processing order) reaching the maximum
+  int B = bestK >> 18, C = best_col, ML = bestK & 0xFFFF;
+  for (uint32_t k = 1; k < a.G; ++k) {
+    const int src = (int)(g * a.G + k);
+    const int ok = __shfl(bestK, src), oc = __shfl(best_col, src);
+    const int ob = ok >> 18;
+    if (ob > B || (ob == B && ob > 0 && oc < C)) { B = ob; C = oc; ML = ok & 0xFFFF; }
+  }
+  if (valid && i == 0) {
+    a.out_start[hit] = p0 - (uint32_t)C;
+    a.out_ml[hit] = ((uint32_t)ML >> 7) << 8 | ((uint32_t)ML & 0x7Fu);
   }
   WaveAddCells(a.cells, (valid && i == 0) ? (unsigned long long)ncols * a.L : 0ull);
 }

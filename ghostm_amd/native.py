@@ -55,6 +55,8 @@ class GhostmStats(ctypes.Structure):
         ("seed_bytes", c_uint64),
         ("score_launches_packed", c_uint64),
         ("score_launches_half", c_uint64),
+        ("traceback_launches", c_uint64),
+        ("traceback_launches_key", c_uint64),
     ]
 
     def as_dict(self) -> dict:

@@ -138,6 +138,8 @@ typedef struct GhostmStats {
   uint64_t seed_bytes;       /* algorithmic bytes of the K1 passes */
   uint64_t score_launches_packed; /* K2 launches that ran a packed 16-bit kernel */
   uint64_t score_launches_half;   /* ... of which the f16 encoding */
+  uint64_t traceback_launches;
+  uint64_t traceback_launches_key; /* K3 launches that ran the key formulation */
 } GhostmStats;
 
 /* Session: parse `aln` options exactly like the reference (getopt string
