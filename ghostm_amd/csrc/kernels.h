@@ -844,11 +844,12 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
   const uint32_t hit = (blockIdx.x * (kTbBlock / 64) + wave) * a.gpw + g;
   const bool valid = g < a.gpw && hit < a.n && a.qid[hit] != 0xFFFFFFFFu;
   uint32_t p0 = 0, width = 0;
-  // byte offset of processing row U = i*S + u's query code inside a table row;
-  // row U walks the query backwards: position Lpad-1-U
-  uint32_t qoff[S];
+  // byte offset (code * 4) of processing row U = i*S + u's query code inside a
+  // table row, four rows per register; row U walks the query backwards:
+  // position Lpad-1-U
+  uint32_t qoff[S / 4];
 #pragma unroll
-  for (int u = 0; u < S; ++u) qoff[u] = kPadCode * 4;
+  for (int w = 0; w < S / 4; ++w) qoff[w] = (kPadCode * 4) * 0x01010101u;
   if (valid) {
     p0 = a.end[hit];
     width = p0 < a.base ? p0 + 1 : a.base;
@@ -856,13 +857,14 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
 #pragma unroll
     for (int u = 0; u < S; ++u) {
       const int k = (int)a.Lpad - 1 - (int)(i * S + u);
-      if (k >= 0 && k < (int)a.L) qoff[u] = (uint32_t)qs[k] * 4;
+      const uint32_t off = (k >= 0 && k < (int)a.L) ? (uint32_t)qs[k] * 4 : kPadCode * 4;
+      qoff[u >> 2] = (qoff[u >> 2] & ~(0xFFu << (8 * (u & 3)))) | (off << (8 * (u & 3)));
     }
   }
   int K[S], KE[S];
 #pragma unroll
   for (int u = 0; u < S; ++u) { K[u] = 0; KE[u] = 0; }
-  int bestK = 0, bestX = (int)kKeyLow, best_col = 0;
+  int bestK = 0, best_col = 0;
   int kout = 0, kfout = 0, kprev = 0;
   bool done = false;
   uint32_t ncols = 0;
@@ -892,9 +894,10 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
         // diagonal keys of the chunk from the previous column first, so the rows
         // below overwrite K in place
         int ks[4];
+        const uint32_t qw = qoff[k >> 2];
 #pragma unroll
         for (int v = 0; v < 4; ++v)
-          ks[v] = (v == 0 ? kd : K[k + v - 1]) + *reinterpret_cast<const int *>(rowp + qoff[k + v]);
+          ks[v] = (v == 0 ? kd : K[k + v - 1]) + *reinterpret_cast<const int *>(rowp + ((qw >> (8 * v)) & 0xFFu));
         kd = K[k + 3];
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
@@ -909,7 +912,8 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
           const int kc = (int)((uint32_t)max(max(k1, KE[u]), KF) & ~kKeyPrio);
           K[u] = kc;
           kup = kc;
-          if (kc > bestX) { bestK = kc; bestX = kc | (int)kKeyLow; best_col = j; }
+          // strict > on h: the upper words are h << 2 (prio cleared)
+          if ((kc >> 16) > (bestK >> 16)) { bestK = kc; best_col = j; }
         }
       }
       kout = K[S - 1];
