@@ -50,6 +50,7 @@ struct DeviceTimes {
   uint64_t score_launches = 0, score_launches_packed = 0, score_launches_half = 0;
   uint64_t score_cells = 0, traceback_cells = 0;
   uint64_t traceback_launches = 0, traceback_launches_key = 0;
+  uint64_t seed_launches_hash = 0;  // Seed() calls whose slot pass used k_seed_hash
 };
 
 class DeviceModule {

@@ -266,6 +266,23 @@ static void LaunchSeed(const kern::SeedArgs &a, uint32_t items, hipStream_t s) {
   hipLaunchKernelGGL((kern::k_seed<B, C, G>), dim3(items), dim3(B), lds, s, a);
 }
 
+// Slot pass of the three LDS classes: the hash-count kernel (table = 2 x cap).
+static void LaunchSeedHashClass(int cls, const kern::SeedArgs &a, uint32_t items, hipStream_t s) {
+  if (items == 0) return;
+  switch (cls) {
+    case 0:
+      hipLaunchKernelGGL((kern::k_seed_hash<256, 8192>), dim3(items), dim3(256), 8192 * 4, s, a);
+      break;
+    case 1:
+      hipLaunchKernelGGL((kern::k_seed_hash<512, 16384>), dim3(items), dim3(512), 16384 * 4, s, a);
+      break;
+    default:
+      hipLaunchKernelGGL((kern::k_seed_hash<1024, 32768>), dim3(items), dim3(1024), 32768 * 4, s, a);
+      break;
+  }
+  HIP_CHECK(hipGetLastError());
+}
+
 static void LaunchSeedClass(int cls, const kern::SeedArgs &a, uint32_t items, hipStream_t s) {
   if (items == 0) return;
   switch (cls) {
@@ -365,16 +382,23 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
   a.slot_cap = kSlotCap;
   a.gbuf = I.gbuf.as<uint32_t>();
   a.gbuf_off = I.gbuf_off.as<unsigned long long>();
-  // K1b pass 1: every class, candidates into per-query slots (largest first)
+  // K1b pass 1: every class, candidates into per-query slots (largest first).
+  // The LDS classes count bins in a hash table when every bin fits 24 bits
+  // (GHOSTM_K1=merge keeps the merge kernel).
+  const char *k1 = getenv("GHOSTM_K1");
+  const bool hash = !(k1 && strcmp(k1, "merge") == 0) && d->len > 0 &&
+                    ((uint64_t)(d->len - 1) >> cfg.log_region) + 2 < (1ull << 24);
   {
     size_t at = list_total;
     for (int c = 3; c >= 0; --c) {
       at -= cls[c].size();
       kern::SeedArgs b = a;
       b.query_list = I.qlist.as<uint32_t>() + at;
-      LaunchSeedClass(c, b, (uint32_t)cls[c].size(), S(stream_));
+      if (hash && c < 3) LaunchSeedHashClass(c, b, (uint32_t)cls[c].size(), S(stream_));
+      else LaunchSeedClass(c, b, (uint32_t)cls[c].size(), S(stream_));
     }
   }
+  times_.seed_launches_hash += hash ? 1 : 0;
   HIP_CHECK(hipMemcpyAsync(counts->data(), I.counts.p, (size_t)nq * 4, hipMemcpyDeviceToHost, S(stream_)));
   HIP_CHECK(hipStreamSynchronize(S(stream_)));
 

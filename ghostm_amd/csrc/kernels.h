@@ -41,6 +41,7 @@ constexpr int kNeg = -30000;           // score of a padding row (keeps it at 0)
 //     LDS (or global buffers for oversized queries), run-length emission.
 constexpr uint32_t kMaxLists = 128;
 constexpr uint32_t kOverflow = 0xFFFFFFFFu;
+constexpr uint32_t kMaxSlotCap = 256;  // slot pass: candidates per query slot
 
 struct SeedListArgs {
   const uint8_t *qseq;
@@ -307,6 +308,115 @@ __global__ __launch_bounds__(BLOCK) void k_seed(SeedArgs a) {
       if (oq) oq[at] = q;
       ++at;
     }
+  }
+}
+
+// K1b' k_seed_hash<BLOCK, TSLOTS>: the slot pass (queries with <= slot_cap
+//     candidates) without sorting the bins. Each wave walks whole lists, one
+//     position per lane; a position whose bin repeats the previous one of its
+//     list is skipped (each list counts once per bin), the others are counted in
+//     an LDS hash table keyed by bin (linear probing, (bin+1) << 8 | count). A
+//     table scan applies c(b) + c(b+1) >= T, the emitted bins (<= slot_cap) are
+//     ranked by value and written in ascending order. Same output as k_seed in
+//     slot mode; queries with more candidates only get their count here and
+//     are redone by k_seed in offset mode. Needs every bin + 1 < 2^24.
+__device__ inline uint32_t BinHash(uint32_t b) { return b * 2654435761u; }
+
+template <uint32_t TSLOTS>
+__device__ inline uint32_t BinCount(const uint32_t *tab, uint32_t b) {
+  const uint32_t key = (b + 1) << 8;
+  uint32_t h = BinHash(b) >> (32 - __builtin_ctz(TSLOTS));
+  while (true) {
+    const uint32_t v = tab[h];
+    if (v == 0) return 0;
+    if ((v & ~0xFFu) == key) return v & 0xFFu;
+    h = (h + 1) & (TSLOTS - 1);
+  }
+}
+
+template <uint32_t BLOCK, uint32_t TSLOTS>
+__global__ __launch_bounds__(BLOCK) void k_seed_hash(SeedArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];  // TSLOTS words (dynamic)
+  __shared__ uint32_t s_emit[kMaxSlotCap];
+  __shared__ uint32_t s_part[BLOCK / 64];
+  __shared__ uint32_t s_total;
+  constexpr uint32_t kPer = TSLOTS / BLOCK;
+  static_assert(kPer <= 32, "emission mask is 32 bits");
+
+  const uint32_t q = a.query_list[blockIdx.x];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t nl = a.nlists;
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) s_tab[tid + k * BLOCK] = 0;
+  __syncthreads();
+
+  // 1. count: wave w takes lists w, w + BLOCK/64, ...
+  for (uint32_t j = wave; j < nl; j += BLOCK / 64) {
+    const uint32_t beg = a.list_beg[(size_t)q * nl + j];
+    const uint32_t len = a.list_len[(size_t)q * nl + j];
+    const uint32_t d0 = j * a.shift;
+    uint32_t carry = 0xFFFFFFFFu;  // last bin of the previous chunk (none yet)
+    for (uint32_t r0 = 0; r0 < len; r0 += 64) {
+      const uint32_t r = r0 + lane;
+      const bool ok = r < len;
+      const uint32_t bin = ok ? (a.positions[beg + r] - d0) >> a.log_region : 0xFFFFFFFEu;
+      uint32_t prev = __shfl_up(bin, 1);
+      if (lane == 0) prev = carry;
+      carry = __shfl(bin, 63);
+      if (ok && bin != prev) {
+        const uint32_t key = (bin + 1) << 8;
+        uint32_t h = BinHash(bin) >> (32 - __builtin_ctz(TSLOTS));
+        while (true) {
+          const uint32_t old = atomicCAS(&s_tab[h], 0u, key | 1u);
+          if (old == 0) break;
+          if ((old & ~0xFFu) == key) {
+            atomicAdd(&s_tab[h], 1u);
+            break;
+          }
+          h = (h + 1) & (TSLOTS - 1);
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // 2. emission test per occupied slot; the phantom bin 0 (c(0) = 0, c(1) >= T)
+  const uint32_t thr = a.threshold;
+  uint32_t mask = 0, mine = 0;
+  bool phantom = false;
+  if (thr != 0) {
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) {
+      const uint32_t v = s_tab[tid + k * BLOCK];
+      if (v == 0) continue;
+      const uint32_t b = (v >> 8) - 1;
+      if ((v & 0xFFu) + BinCount<TSLOTS>(s_tab, b + 1) >= thr) {
+        mask |= 1u << k;
+        ++mine;
+      }
+    }
+    if (tid == 0 && BinCount<TSLOTS>(s_tab, 0) == 0 && BinCount<TSLOTS>(s_tab, 1) >= thr) {
+      phantom = true;
+      ++mine;
+    }
+  }
+  const uint32_t base = BlockExclusiveScan(mine, s_part, &s_total);
+  const uint32_t total = s_total;
+  if (tid == 0) a.counts[q] = total;
+  if (total == 0 || total > a.slot_cap) return;  // offset pass redoes the wide ones
+
+  // 3. emitted bins -> LDS, rank by value (all distinct), write in order
+  uint32_t at = base;
+  if (phantom) s_emit[at++] = 0;
+  for (uint32_t k = 0; k < kPer; ++k)
+    if (mask & (1u << k)) s_emit[at++] = (s_tab[tid + k * BLOCK] >> 8) - 1;
+  __syncthreads();
+  uint32_t *os = a.slots + (size_t)q * a.slot_cap;
+  for (uint32_t e = tid; e < total; e += BLOCK) {
+    const uint32_t b = s_emit[e];
+    uint32_t rank = 0;
+    for (uint32_t k = 0; k < total; ++k) rank += s_emit[k] < b ? 1u : 0u;
+    os[rank] = b << a.log_region;
   }
 }
 

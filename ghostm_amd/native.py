@@ -57,6 +57,7 @@ class GhostmStats(ctypes.Structure):
         ("score_launches_half", c_uint64),
         ("traceback_launches", c_uint64),
         ("traceback_launches_key", c_uint64),
+        ("seed_runs_hash", c_uint64),
     ]
 
     def as_dict(self) -> dict:

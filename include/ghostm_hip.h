@@ -140,6 +140,7 @@ typedef struct GhostmStats {
   uint64_t score_launches_half;   /* ... of which the f16 encoding */
   uint64_t traceback_launches;
   uint64_t traceback_launches_key; /* K3 launches that ran the key formulation */
+  uint64_t seed_runs_hash;        /* K1 runs whose slot pass used the hash-count kernel */
 } GhostmStats;
 
 /* Session: parse `aln` options exactly like the reference (getopt string

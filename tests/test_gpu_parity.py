@@ -178,7 +178,7 @@ def test_reference_gpu_batching_rule(dataset):
     lib.FreeGpu()
 
 
-@pytest.mark.parametrize("kind", ["int32", "int16", "k3_int32"])
+@pytest.mark.parametrize("kind", ["int32", "int16", "k3_int32", "k1_merge"])
 @pytest.mark.parametrize("ds,var,opts", [("syn_small", "default", []), ("syn_short", "default", []),
                                          ("syn_small", "r64_pam250", ["-r", "64", "-M", cases.PAM250, "-y", "2"])])
 def test_forced_score_encoding_matches_golden(kind, ds, var, opts, dataset, golden, tmp_path):
@@ -186,13 +186,16 @@ def test_forced_score_encoding_matches_golden(kind, ds, var, opts, dataset, gold
     scores fit f16's exact-integer range, the int16 one above that, int32 when
     scores may exceed int16. Forced with GHOSTM_K2 each reproduces the golden."""
     d = dataset(ds)
-    env = {"GHOSTM_K3": "int32"} if kind == "k3_int32" else {"GHOSTM_K2": kind}
+    env = ({"GHOSTM_K3": "int32"} if kind == "k3_int32" else
+           {"GHOSTM_K1": "merge"} if kind == "k1_merge" else {"GHOSTM_K2": kind})
     text, st = _gpu_text(d, opts, env, str(tmp_path / "g.out"))
     (tmp_path / "g.out").write_bytes(text)
     assert cases.sha256(str(tmp_path / "g.out")) == golden["aln"][f"{ds}/{var}"]["sha256"]
     assert st["traceback_launches"] > 0
     if kind == "k3_int32":
         assert st["traceback_launches_key"] == 0
+    elif kind == "k1_merge":
+        assert st["seed_runs_hash"] == 0
     else:
         assert st["score_launches"] > 0 and st["score_launches_half"] == 0
         assert st["score_launches_packed"] == (st["score_launches"] if kind == "int16" else 0)
@@ -203,6 +206,7 @@ def test_default_encoding_is_f16_when_scores_fit(dataset, golden, tmp_path):
     text, st = _gpu_text(d, [], {}, str(tmp_path / "g.out"))
     assert st["score_launches_half"] == st["score_launches"] > 0
     assert st["traceback_launches_key"] == st["traceback_launches"] > 0
+    assert st["seed_runs_hash"] > 0
     text2, st2 = _gpu_text(d, ["-M", cases.PAM250, "-G", "8", "-E", "1", "-y", "2"], {},
                             str(tmp_path / "p.out"))
     assert st2["score_launches_half"] == 0 and st2["score_launches_packed"] == st2["score_launches"]
