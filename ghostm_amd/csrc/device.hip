@@ -266,18 +266,18 @@ static void LaunchSeed(const kern::SeedArgs &a, uint32_t items, hipStream_t s) {
   hipLaunchKernelGGL((kern::k_seed<B, C, G>), dim3(items), dim3(B), lds, s, a);
 }
 
-// Slot pass of the three LDS classes: the hash-count kernel (table = 2 x cap).
+// Slot pass of the three LDS classes: the hash-count kernel (table >= 1.5 x cap).
 static void LaunchSeedHashClass(int cls, const kern::SeedArgs &a, uint32_t items, hipStream_t s) {
   if (items == 0) return;
   switch (cls) {
     case 0:
       hipLaunchKernelGGL((kern::k_seed_hash<256, 8192>), dim3(items), dim3(256), 8192 * 4, s, a);
       break;
-    case 1:
-      hipLaunchKernelGGL((kern::k_seed_hash<512, 16384>), dim3(items), dim3(512), 16384 * 4, s, a);
+    case 1:  // load <= 2/3: 48 KB, three workgroups per CU
+      hipLaunchKernelGGL((kern::k_seed_hash<512, 12288>), dim3(items), dim3(512), 12288 * 4, s, a);
       break;
     default:
-      hipLaunchKernelGGL((kern::k_seed_hash<1024, 32768>), dim3(items), dim3(1024), 32768 * 4, s, a);
+      hipLaunchKernelGGL((kern::k_seed_hash<1024, 24576>), dim3(items), dim3(1024), 24576 * 4, s, a);
       break;
   }
   HIP_CHECK(hipGetLastError());

@@ -322,59 +322,119 @@ __global__ __launch_bounds__(BLOCK) void k_seed(SeedArgs a) {
 //     are redone by k_seed in offset mode. Needs every bin + 1 < 2^24.
 __device__ inline uint32_t BinHash(uint32_t b) { return b * 2654435761u; }
 
+// Linear probing over slots, read eight at a time: a window is two 4-slot
+// buckets (two 128-bit LDS reads), windows advance by two buckets, wrapping at
+// the table end — the same slot order for inserts and lookups. At load <= 2/3
+// almost every lookup, found or not, ends in its first window.
 template <uint32_t TSLOTS>
-__device__ inline uint32_t BinCount(const uint32_t *tab, uint32_t b) {
-  const uint32_t key = (b + 1) << 8;
-  uint32_t h = BinHash(b) >> (32 - __builtin_ctz(TSLOTS));
-  while (true) {
-    const uint32_t v = tab[h];
-    if (v == 0) return 0;
-    if ((v & ~0xFFu) == key) return v & 0xFFu;
-    h = (h + 1) & (TSLOTS - 1);
+struct BinTable {
+  static constexpr uint32_t kBuckets = TSLOTS / 4;
+  uint32_t *tab;
+  __device__ static uint32_t Bucket(uint32_t b) { return __umulhi(BinHash(b), kBuckets); }
+  __device__ static uint32_t Next(uint32_t k) { return k + 1 == kBuckets ? 0u : k + 1; }
+  // slots of window k in probe order
+  __device__ void Window(uint32_t k, uint32_t sl[8], uint32_t *k1) const {
+    *k1 = Next(k);
+    const uint4 w0 = reinterpret_cast<const uint4 *>(tab)[k];
+    const uint4 w1 = reinterpret_cast<const uint4 *>(tab)[*k1];
+    sl[0] = w0.x; sl[1] = w0.y; sl[2] = w0.z; sl[3] = w0.w;
+    sl[4] = w1.x; sl[5] = w1.y; sl[6] = w1.z; sl[7] = w1.w;
   }
-}
+  // first slot of the window holding `key` or empty: 0..7, or 8 if none
+  __device__ static uint32_t FirstMatch(const uint32_t sl[8], uint32_t key, bool *found) {
+    uint32_t pos = 8;
+    *found = false;
+#pragma unroll
+    for (int m = 7; m >= 0; --m) {
+      const bool hitk = (sl[m] & ~0xFFu) == key;
+      if (hitk || sl[m] == 0) { pos = (uint32_t)m; *found = hitk; }
+    }
+    return pos;
+  }
+  __device__ uint32_t Count(uint32_t b) const {
+    const uint32_t key = (b + 1) << 8;
+    uint32_t k = Bucket(b);
+    while (true) {
+      uint32_t sl[8], k1;
+      Window(k, sl, &k1);
+      bool found;
+      const uint32_t pos = FirstMatch(sl, key, &found);
+      if (pos < 8) return found ? (sl[pos] & 0xFFu) : 0u;
+      k = Next(k1);
+    }
+  }
+  __device__ void Insert(uint32_t b) {
+    const uint32_t key = (b + 1) << 8;
+    uint32_t k = Bucket(b);
+    while (true) {
+      uint32_t sl[8], k1;
+      Window(k, sl, &k1);
+      bool found;
+      const uint32_t pos = FirstMatch(sl, key, &found);
+      if (pos == 8) {
+        k = Next(k1);
+        continue;
+      }
+      uint32_t *slot = tab + (pos < 4 ? k * 4 + pos : k1 * 4 + (pos - 4));
+      if (found) {
+        atomicAdd(slot, 1u);
+        return;
+      }
+      const uint32_t old = atomicCAS(slot, 0u, key | 1u);
+      if (old == 0) return;
+      if ((old & ~0xFFu) == key) {
+        atomicAdd(slot, 1u);
+        return;
+      }
+      // another bin took the slot first: look at the same window again
+    }
+  }
+};
 
 template <uint32_t BLOCK, uint32_t TSLOTS>
 __global__ __launch_bounds__(BLOCK) void k_seed_hash(SeedArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];  // TSLOTS words (dynamic)
-  __shared__ uint32_t s_emit[kMaxSlotCap];
+  __shared__ __attribute__((aligned(16))) uint32_t s_emit[kMaxSlotCap];
   __shared__ uint32_t s_part[BLOCK / 64];
   __shared__ uint32_t s_total;
   constexpr uint32_t kPer = TSLOTS / BLOCK;
-  static_assert(kPer <= 32, "emission mask is 32 bits");
+  static_assert(kPer <= 32 && kPer * BLOCK == TSLOTS && TSLOTS % 8 == 0, "table shape");
 
   const uint32_t q = a.query_list[blockIdx.x];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t nl = a.nlists;
 #pragma unroll
   for (uint32_t k = 0; k < kPer; ++k) s_tab[tid + k * BLOCK] = 0;
+  BinTable<TSLOTS> table{s_tab};
   __syncthreads();
 
-  // 1. count: wave w takes lists w, w + BLOCK/64, ...
-  for (uint32_t j = wave; j < nl; j += BLOCK / 64) {
-    const uint32_t beg = a.list_beg[(size_t)q * nl + j];
-    const uint32_t len = a.list_len[(size_t)q * nl + j];
-    const uint32_t d0 = j * a.shift;
-    uint32_t carry = 0xFFFFFFFFu;  // last bin of the previous chunk (none yet)
-    for (uint32_t r0 = 0; r0 < len; r0 += 64) {
+  // 1. count: wave w takes lists in groups of four (four independent position
+  //    loads in flight per lane), groups w, w + BLOCK/64, ...
+  constexpr uint32_t kLG = 4;
+  for (uint32_t j0 = wave * kLG; j0 < nl; j0 += (BLOCK / 64) * kLG) {
+    uint32_t beg[kLG], len[kLG], d0[kLG], carry[kLG], maxlen = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < kLG; ++t) {
+      const uint32_t j = j0 + t;
+      beg[t] = j < nl ? a.list_beg[(size_t)q * nl + j] : 0;
+      len[t] = j < nl ? a.list_len[(size_t)q * nl + j] : 0;
+      d0[t] = j * a.shift;
+      carry[t] = 0xFFFFFFFFu;  // last bin of the list's previous chunk (none yet)
+      maxlen = max(maxlen, len[t]);
+    }
+    for (uint32_t r0 = 0; r0 < maxlen; r0 += 64) {
       const uint32_t r = r0 + lane;
-      const bool ok = r < len;
-      const uint32_t bin = ok ? (a.positions[beg + r] - d0) >> a.log_region : 0xFFFFFFFEu;
-      uint32_t prev = __shfl_up(bin, 1);
-      if (lane == 0) prev = carry;
-      carry = __shfl(bin, 63);
-      if (ok && bin != prev) {
-        const uint32_t key = (bin + 1) << 8;
-        uint32_t h = BinHash(bin) >> (32 - __builtin_ctz(TSLOTS));
-        while (true) {
-          const uint32_t old = atomicCAS(&s_tab[h], 0u, key | 1u);
-          if (old == 0) break;
-          if ((old & ~0xFFu) == key) {
-            atomicAdd(&s_tab[h], 1u);
-            break;
-          }
-          h = (h + 1) & (TSLOTS - 1);
-        }
+      uint32_t pos[kLG];
+#pragma unroll
+      for (uint32_t t = 0; t < kLG; ++t) pos[t] = r < len[t] ? a.positions[beg[t] + r] : 0u;
+#pragma unroll
+      for (uint32_t t = 0; t < kLG; ++t) {
+        const bool ok = r < len[t];
+        const uint32_t bin = ok ? (pos[t] - d0[t]) >> a.log_region : 0xFFFFFFFEu;
+        uint32_t prev = __shfl_up(bin, 1);
+        if (lane == 0) prev = carry[t];
+        carry[t] = __shfl(bin, 63);
+        if (ok && bin != prev) table.Insert(bin);
       }
     }
   }
@@ -390,12 +450,12 @@ __global__ __launch_bounds__(BLOCK) void k_seed_hash(SeedArgs a) {
       const uint32_t v = s_tab[tid + k * BLOCK];
       if (v == 0) continue;
       const uint32_t b = (v >> 8) - 1;
-      if ((v & 0xFFu) + BinCount<TSLOTS>(s_tab, b + 1) >= thr) {
+      if ((v & 0xFFu) + table.Count(b + 1) >= thr) {
         mask |= 1u << k;
         ++mine;
       }
     }
-    if (tid == 0 && BinCount<TSLOTS>(s_tab, 0) == 0 && BinCount<TSLOTS>(s_tab, 1) >= thr) {
+    if (tid == 0 && table.Count(0) == 0 && table.Count(1) >= thr) {
       phantom = true;
       ++mine;
     }
@@ -410,13 +470,27 @@ __global__ __launch_bounds__(BLOCK) void k_seed_hash(SeedArgs a) {
   if (phantom) s_emit[at++] = 0;
   for (uint32_t k = 0; k < kPer; ++k)
     if (mask & (1u << k)) s_emit[at++] = (s_tab[tid + k * BLOCK] >> 8) - 1;
+  // pad to a multiple of 16 with values above every bin (ranks unaffected)
+  for (uint32_t e = total + tid; e < ((total + 15) & ~15u); e += BLOCK) s_emit[e] = 0xFFFFFFFFu;
   __syncthreads();
+  // rank of element e = number of smaller ones; four lanes per element, each
+  // counting a quarter of the array with 128-bit reads
   uint32_t *os = a.slots + (size_t)q * a.slot_cap;
-  for (uint32_t e = tid; e < total; e += BLOCK) {
-    const uint32_t b = s_emit[e];
+  const uint32_t n16 = (total + 15) >> 4;  // 16-element blocks
+  for (uint32_t base4 = 0; base4 < total * 4; base4 += BLOCK) {
+    const uint32_t t4 = base4 + tid;
+    const uint32_t e = t4 >> 2, part = t4 & 3;
+    const uint32_t b = e < total ? s_emit[e] : 0u;
     uint32_t rank = 0;
-    for (uint32_t k = 0; k < total; ++k) rank += s_emit[k] < b ? 1u : 0u;
-    os[rank] = b << a.log_region;
+    if (e < total) {
+      for (uint32_t blk = 0; blk < n16; ++blk) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(s_emit + blk * 16 + part * 4);
+        rank += (v.x < b) + (v.y < b) + (v.z < b) + (v.w < b);
+      }
+    }
+    rank += __shfl_xor(rank, 1);
+    rank += __shfl_xor(rank, 2);
+    if (e < total && part == 0) os[rank] = b << a.log_region;
   }
 }
 
