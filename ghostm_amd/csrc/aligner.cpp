@@ -220,13 +220,6 @@ Session::Session(const AlignerOptions &opt) : opt_(opt) {
   formatter_.reset(new TaskQueue());
 }
 
-Session::~Session() {
-  formatter_.reset();
-  DeviceModule &dev = DeviceModule::Get();
-  for (QueryData &q : queries_) dev.Free(q.dev);
-  for (DbData &d : dbs_) dev.Free(d.dev);
-}
-
 // The CPU path's batch cuts (aligner.cpp:383-521 driven by Execute's loop at
 // 131-171): a query whose candidates push the running total above -l is carried
 // into the next batch; the loop stops at the first empty batch, so a carried last
@@ -471,55 +464,139 @@ void Session::RunQueryChunk(QueryData &q) {
 
 // ------------------------------------------------------------------ output
 namespace {
-inline void AppendU32(std::string *s, uint32_t v) {
-  char buf[16];
-  int n = 0;
-  do { buf[n++] = (char)('0' + v % 10); v /= 10; } while (v);
-  while (n) s->push_back(buf[--n]);
+// two-digit table for integer formatting
+struct Digits {
+  char d[200];
+  Digits() {
+    for (int i = 0; i < 100; ++i) { d[2 * i] = (char)('0' + i / 10); d[2 * i + 1] = (char)('0' + i % 10); }
+  }
+};
+const Digits kDigits;
+
+inline char *PutU32(char *p, uint32_t v) {
+  char buf[12];
+  char *e = buf + sizeof(buf), *b = e;
+  while (v >= 100) {
+    const uint32_t r = v % 100;
+    v /= 100;
+    b -= 2;
+    std::memcpy(b, kDigits.d + 2 * r, 2);
+  }
+  if (v >= 10) {
+    b -= 2;
+    std::memcpy(b, kDigits.d + 2 * v, 2);
+  } else {
+    *--b = (char)('0' + v);
+  }
+  std::memcpy(p, b, (size_t)(e - b));
+  return p + (e - b);
 }
 // ostream << float == printf("%g") == to_chars(general, 6) (checked on 6e8 bit
 // patterns incl. NaN/inf/denormals), and to_chars is ~5x faster than snprintf.
-inline void AppendFloat(std::string *s, float f) {
-  char buf[48];
-  const auto r = std::to_chars(buf, buf + sizeof(buf), f, std::chars_format::general, 6);
-  s->append(buf, r.ptr - buf);
+inline char *PutFloat(char *p, float f) {
+  return std::to_chars(p, p + 48, f, std::chars_format::general, 6).ptr;
 }
+inline char *PutStr(char *p, const std::string &s) {
+  std::memcpy(p, s.data(), s.size());
+  return p + s.size();
+}
+inline std::string FloatText(float f) {
+  char buf[48];
+  return std::string(buf, PutFloat(buf, f));
+}
+constexpr uint32_t kIdLen = 512, kIdMatch = 128;
+}  // namespace
 
-// One output line, WriteOutput / V1 / V2 (aligner.cpp:951-1012).
-struct LineWriter {
-  int style;
+// One output line, WriteOutput / V1 / V2 (aligner.cpp:951-1012). Everything that
+// depends only on the score (bits, exp(-lambda*s)) or only on (len, matches)
+// (the identity) is formatted once per session; per hit only the E-value is
+// computed and formatted, with the reference's float/double steps.
+struct LineFormat {
+  int style = 0;
   EvalueCalculator ev;
-  void Write(std::string *s, const std::string &qname, const std::string &sname, uint32_t score,
-             uint32_t start, uint32_t end, uint32_t len, uint32_t match, float seq_id,
-             uint64_t space) const {
-    s->append(qname);
-    s->push_back('\t');
-    s->append(sname);
-    s->push_back('\t');
-    if (style == 1) {
-      AppendU32(s, score); s->push_back('\t');
-      AppendU32(s, start + 1); s->push_back('\t');
-      AppendU32(s, end + 1);
-    } else if (style == 2) {
-      AppendU32(s, score); s->push_back('\t');
-      AppendU32(s, start + 1); s->push_back('\t');
-      AppendU32(s, end + 1); s->push_back('\t');
-      AppendFloat(s, seq_id); s->push_back('\t');
-      AppendU32(s, len); s->push_back('\t');
-      AppendU32(s, match);
-    } else {
-      AppendFloat(s, seq_id * 100); s->push_back('\t');
-      AppendU32(s, len); s->push_back('\t');
-      AppendU32(s, match); s->push_back('\t');
-      AppendU32(s, start + 1); s->push_back('\t');
-      AppendU32(s, end + 1); s->push_back('\t');
-      AppendFloat(s, ev.Evalue((int)score, space)); s->push_back('\t');
-      AppendFloat(s, ev.Bits((int)score)); s->push_back('\t');
+  std::vector<std::string> bits_txt;  // per score
+  std::vector<double> expd;           // per score: exp(-1.0 * s * lambda)
+  std::vector<std::string> id_txt;    // per (len, match): 100*id (style 0) or id (style 2)
+
+  LineFormat(int st, const KarlinParams &k, uint32_t max_score) : style(st), ev(k) {
+    if (style == 0) {
+      bits_txt.resize(max_score + 1);
+      expd.resize(max_score + 1);
+      for (uint32_t sc = 0; sc <= max_score; ++sc) {
+        bits_txt[sc] = FloatText(ev.Bits((int)sc));
+        expd[sc] = exp(static_cast<double>(-1.0 * (int)sc * ev.p.lambda));
+      }
     }
-    s->push_back('\n');
+    if (style != 1) {
+      id_txt.resize(kIdLen * kIdMatch);
+      for (uint32_t len = 1; len < kIdLen; ++len)
+        for (uint32_t m = 0; m < kIdMatch && m <= len; ++m) id_txt[len * kIdMatch + m] = FloatText(Id(len, m));
+    }
+  }
+  float Id(uint32_t len, uint32_t m) const {
+    const float id = (float)m / (float)len;  // aligner.cpp:945
+    return style == 0 ? id * 100 : id;
+  }
+  char *PutId(char *p, uint32_t len, uint32_t m) const {
+    if (len < kIdLen && m < kIdMatch && m <= len && len > 0) return PutStr(p, id_txt[len * kIdMatch + m]);
+    return PutFloat(p, Id(len, m));
+  }
+  // bytes a line can take beyond the two names
+  static constexpr size_t kFixed = 160;
+  // scaled = (float)search_space * K, per query
+  char *Write(char *p, const std::string &qname, const std::string &sname, uint32_t score, uint32_t start,
+              uint32_t end, uint32_t len, uint32_t match, float scaled) const {
+    p = PutStr(p, qname);
+    *p++ = '\t';
+    p = PutStr(p, sname);
+    *p++ = '\t';
+    if (style == 1) {
+      p = PutU32(p, score); *p++ = '\t';
+      p = PutU32(p, start + 1); *p++ = '\t';
+      p = PutU32(p, end + 1);
+    } else if (style == 2) {
+      p = PutU32(p, score); *p++ = '\t';
+      p = PutU32(p, start + 1); *p++ = '\t';
+      p = PutU32(p, end + 1); *p++ = '\t';
+      p = PutId(p, len, match); *p++ = '\t';
+      p = PutU32(p, len); *p++ = '\t';
+      p = PutU32(p, match);
+    } else {
+      p = PutId(p, len, match); *p++ = '\t';
+      p = PutU32(p, len); *p++ = '\t';
+      p = PutU32(p, match); *p++ = '\t';
+      p = PutU32(p, start + 1); *p++ = '\t';
+      p = PutU32(p, end + 1); *p++ = '\t';
+      const double e = score < expd.size() ? expd[score] : exp(static_cast<double>(-1.0 * (int)score * ev.p.lambda));
+      p = PutFloat(p, (float)((double)scaled * e)); *p++ = '\t';
+      if (score < bits_txt.size()) p = PutStr(p, bits_txt[score]);
+      else p = PutFloat(p, ev.Bits((int)score));
+      *p++ = '\t';
+    }
+    *p++ = '\n';
+    return p;
   }
 };
+
+namespace {
+// Appends lines through a raw cursor into a std::string that grows in chunks.
+struct TextCursor {
+  std::string &s;
+  size_t used;
+  explicit TextCursor(std::string &str) : s(str), used(str.size()) {}
+  char *Reserve(size_t need) {
+    if (s.size() < used + need) s.resize(std::max(used + need, s.size() * 2 + 4096));
+    return &s[used];
+  }
+  void Commit(char *end) { used = (size_t)(end - s.data()); }
+  ~TextCursor() { s.resize(used); }
+};
 }  // namespace
+
+const LineFormat &Session::Format() {
+  if (!format_) format_.reset(new LineFormat(opt_.output_style, opt_.karlin, 4095));
+  return *format_;
+}
 
 void Session::Part::Reset(size_t pieces) {
   text.resize(pieces);
@@ -536,16 +613,19 @@ Session::Part *Session::NewPart() {
 void Session::FormatResults(const QueryData &q, const Results &results, Part *out) {
   const uint32_t n = q.chunk.nseq;
   out->Reset(threads_);
-  const LineWriter w{opt_.output_style, EvalueCalculator(opt_.karlin)};
+  const LineFormat &w = Format();
   ParallelFor(n, threads_, [&](size_t b, size_t e, unsigned t) {
-    std::string &text = out->text[t];
+    TextCursor text(out->text[t]);
     std::vector<GhostmHit> &hits = out->hits[t];
     for (size_t i = b; i < e; ++i) {
       const uint64_t space = (uint64_t)q.qlen[i] * (uint64_t)db_sum_u32_;
+      const float scaled = (float)space * w.ev.p.K;
+      const std::string &qname = q.chunk.names[i];
       for (const HitRecord &h : results[i]) {
         const DbData &d = dbs_[h.db_chunk];
-        w.Write(&text, q.chunk.names[i], d.chunk.names[h.subject], h.score, h.start, h.end, h.aln_len,
-                h.aln_match, h.seq_id, space);
+        const std::string &sname = d.chunk.names[h.subject];
+        char *p = text.Reserve(qname.size() + sname.size() + LineFormat::kFixed);
+        text.Commit(w.Write(p, qname, sname, h.score, h.start, h.end, h.aln_len, h.aln_match, scaled));
         hits.push_back(GhostmHit{q.global_base + (uint32_t)i, d.global_base + h.subject, h.score, h.start,
                                  h.end, h.aln_len, h.aln_match, h.seq_id});
       }
@@ -560,24 +640,27 @@ void Session::FormatSelected(const QueryData &q, uint32_t g0, const std::vector<
   const uint32_t ng = (uint32_t)counts.size();
   const unsigned workers = std::max(1u, threads_ > 1 ? threads_ - 1 : 1u);
   out->Reset(workers);
-  const LineWriter w{opt_.output_style, EvalueCalculator(opt_.karlin)};
+  const LineFormat &w = Format();
   const DbData &d = dbs_[0];
   ParallelFor(ng, workers, [&](size_t b, size_t e, unsigned t) {
-    std::string &text = out->text[t];
     std::vector<GhostmHit> &ph = out->hits[t];
     size_t nh = 0;
     for (size_t g = b; g < e; ++g) nh += counts[g];
-    text.reserve(nh * 96);
+    out->text[t].reserve(nh * 96);
     ph.reserve(nh);
+    TextCursor text(out->text[t]);
     for (size_t g = b; g < e; ++g) {
       const uint32_t i = q.group_last[g0 + g];
       const std::string &name = q.chunk.names[i];
       const uint64_t space = (uint64_t)q.qlen[i] * (uint64_t)db_sum_u32_;
+      const float scaled = (float)space * w.ev.p.K;
       for (uint32_t k = 0; k < counts[g]; ++k) {
         const SelectedHit &h = hits[(size_t)g * cap + k];
         const uint32_t len = h.ml >> 8, match = h.ml & 0xFFu;
         const float seq_id = (float)match / (float)len;  // aligner.cpp:945
-        w.Write(&text, name, d.chunk.names[h.sid], h.score, h.start, h.end, len, match, seq_id, space);
+        const std::string &sname = d.chunk.names[h.sid];
+        char *p = text.Reserve(name.size() + sname.size() + LineFormat::kFixed);
+        text.Commit(w.Write(p, name, sname, h.score, h.start, h.end, len, match, scaled));
         ph.push_back(GhostmHit{q.global_base + i, d.global_base + h.sid, h.score, h.start, h.end, len, match,
                                seq_id});
       }
@@ -596,6 +679,7 @@ void Session::Run() {
   joined_valid_ = false;
   hits_.clear();
   hits_valid_ = false;
+  Format();  // built here, before any formatting task can need it
   const double t0 = NowSeconds();
   for (QueryData &q : queries_) {
     RunQueryChunk(q);
@@ -649,6 +733,14 @@ void Session::WriteOutputFile() {
   std::ofstream out(opt_.output_file.c_str(), std::ios::binary);
   for (size_t k = 0; k < used_parts_; ++k)
     for (const std::string &t : parts_[k].text) out.write(t.data(), (std::streamsize)t.size());
+}
+
+// defined after LineFormat (a complete type for format_)
+Session::~Session() {
+  formatter_.reset();
+  DeviceModule &dev = DeviceModule::Get();
+  for (QueryData &q : queries_) dev.Free(q.dev);
+  for (DbData &d : dbs_) dev.Free(d.dev);
 }
 
 }  // namespace ghostm

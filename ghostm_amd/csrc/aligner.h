@@ -26,6 +26,8 @@
 
 namespace ghostm {
 
+struct LineFormat;  // output line writer with per-session caches (aligner.cpp)
+
 // reference AlignerOption (aligner.h:42-61), defaults of SetOption (aligner.cpp:226-243)
 struct AlignerOptions {
   std::string output_file;
@@ -133,6 +135,7 @@ class Session {
   void FormatSelected(const QueryData &q, uint32_t g0, const std::vector<uint32_t> &counts,
                       const std::vector<SelectedHit> &hits, uint32_t cap, Part *out);
   Part *NewPart();
+  const LineFormat &Format();
 
   AlignerOptions opt_;
   std::vector<QueryData> queries_;
@@ -148,6 +151,7 @@ class Session {
   GhostmStats stats_{};
   unsigned threads_ = 1;
   std::unique_ptr<TaskQueue> formatter_;
+  std::unique_ptr<LineFormat> format_;
 };
 
 }  // namespace ghostm
