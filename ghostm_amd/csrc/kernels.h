@@ -1172,11 +1172,14 @@ __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
   unsigned long long *keys = a.keys + b;
   for (unsigned long long i = 0; i < n; ++i)
     keys[i] = ((unsigned long long)a.score[b + i] << 32) | (uint32_t)i;
-  stdsort::Sort(keys, (long)n, ScoreDescending());
+  // std::sort's order, finalized lazily: the walk usually stops long before
+  // the whole group is sorted
+  stdsort::LazySort<unsigned long long, ScoreDescending> order(keys, (long)n, ScoreDescending());
   uint32_t *sid_out = a.sel_sid + (size_t)g * a.cap;
   uint32_t *cand_out = a.sel_cand + (size_t)g * a.cap;
   uint32_t count = 0;
   for (unsigned long long i = 0; i < n; ++i) {
+    while ((long)i >= order.done) order.Advance();
     const unsigned long long c = b + (uint32_t)keys[i];
     const uint32_t sid = SubjectOf(a.subj_start, a.nsubj, a.dblen, a.end[c]);
     bool seen = false;

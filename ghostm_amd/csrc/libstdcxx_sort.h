@@ -170,5 +170,48 @@ template <class T, class Less> GHOSTM_HD void Sort(T *first, long n, Less less) 
   }
 }
 
+// Lazy form of Sort: finalizes the array left to right, one partition at a
+// time, so a caller that only needs a prefix (the Merge walk stops after -b
+// subjects) skips the rest. After Advance() returns true, [first, first + done)
+// holds exactly what std::sort leaves there: introsort's partitions are
+// disjoint and ordered (every element of a left part is not "less" than any of
+// its right part), so the final insertion pass never moves an element across a
+// partition boundary and may be run per partition; a heap-sorted partition is
+// already in order. Right parts wait on a stack; LIFO order is left to right.
+template <class T, class Less> struct LazySort {
+  struct Frame {
+    T *first, *last;
+    int depth;
+  };
+  T *base;
+  Less less;
+  Frame stack[96];
+  int sp = 0;
+  long done = 0;
+  GHOSTM_HD LazySort(T *first, long n, Less l) : base(first), less(l) {
+    if (n > 0) stack[sp++] = Frame{first, first + n, Lg(n) * 2};
+  }
+  GHOSTM_HD bool Advance() {
+    if (sp == 0) return false;
+    Frame f = stack[--sp];
+    while (f.last - f.first > kThreshold) {
+      if (f.depth == 0) {
+        HeapSortRange(f.first, f.last, less);
+        done = f.last - base;
+        return true;
+      }
+      --f.depth;
+      T *mid = f.first + (f.last - f.first) / 2;
+      MoveMedianToFirst(f.first, f.first + 1, mid, f.last - 1, less);
+      T *cut = UnguardedPartition(f.first + 1, f.last, f.first, less);
+      stack[sp++] = Frame{cut, f.last, f.depth};
+      f.last = cut;
+    }
+    InsertionSort(f.first, f.last, less);
+    done = f.last - base;
+    return true;
+  }
+};
+
 }  // namespace stdsort
 }  // namespace ghostm

@@ -19,13 +19,24 @@ int main(int argc, char **argv) {
   std::mt19937_64 rng(12345);
   auto less = [](const Item &a, const Item &b) { return a.score > b.score; };
   long bad = 0, total = 0;
+  long lazy_bad = 0;
   auto check = [&](std::vector<Item> v) {
-    std::vector<Item> a = v, b = v;
+    std::vector<Item> a = v, b = v, c = v;
     std::sort(a.begin(), a.end(), less);
     ghostm::stdsort::Sort(b.data(), (long)b.size(), less);
     ++total;
     for (size_t i = 0; i < a.size(); ++i)
       if (a[i].idx != b[i].idx) { ++bad; return; }
+    // lazy form: every finalized prefix already equals std::sort's
+    ghostm::stdsort::LazySort<Item, decltype(less)> ls(c.data(), (long)c.size(), less);
+    long prev = 0;
+    while (ls.Advance()) {
+      if (ls.done <= prev || ls.done > (long)c.size()) { ++lazy_bad; return; }
+      for (long i = prev; i < ls.done; ++i)
+        if (a[i].idx != c[i].idx) { ++lazy_bad; return; }
+      prev = ls.done;
+    }
+    if (prev != (long)c.size()) ++lazy_bad;
   };
   for (long t = 0; t < trials; ++t) {
     const long n = (long)(rng() % (t % 10 == 0 ? 2000 : 300));
@@ -60,7 +71,8 @@ int main(int argc, char **argv) {
     for (long i = 0; i < n; ++i)
       if (a[i].idx != b[i].idx) { ++heap_bad; break; }
   }
-  bad += heap_bad;
+  bad += heap_bad + lazy_bad;
+  printf("lazy prefixes: %ld mismatches\n", lazy_bad);
   printf("heap fallback: %ld mismatches\n", heap_bad);
   printf("stdsort emulation: %ld arrays, %ld mismatches\n", total, bad);
   return bad != 0;
