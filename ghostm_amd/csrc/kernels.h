@@ -394,6 +394,8 @@ struct BinTable {
 template <uint32_t BLOCK, uint32_t TSLOTS>
 __global__ __launch_bounds__(BLOCK) void k_seed_hash(SeedArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];  // TSLOTS words (dynamic)
+  __shared__ uint32_t s_beg[kMaxLists];
+  __shared__ uint32_t s_off[kMaxLists + 1];
   __shared__ __attribute__((aligned(16))) uint32_t s_emit[kMaxSlotCap];
   __shared__ uint32_t s_part[BLOCK / 64];
   __shared__ uint32_t s_total;
@@ -408,33 +410,54 @@ __global__ __launch_bounds__(BLOCK) void k_seed_hash(SeedArgs a) {
   BinTable<TSLOTS> table{s_tab};
   __syncthreads();
 
-  // 1. count: wave w takes lists in groups of four (four independent position
-  //    loads in flight per lane), groups w, w + BLOCK/64, ...
-  constexpr uint32_t kLG = 4;
-  for (uint32_t j0 = wave * kLG; j0 < nl; j0 += (BLOCK / 64) * kLG) {
-    uint32_t beg[kLG], len[kLG], d0[kLG], carry[kLG], maxlen = 0;
+  // 1. count. The block's lists are concatenated (s_off = prefix of their
+  //    lengths) and cut into 64-entry chunks dealt round-robin to the waves,
+  //    four chunks in flight per wave, so long k-mer lists do not serialise one
+  //    wave. An entry whose bin repeats the previous entry of the same list is
+  //    skipped (each list counts once per bin); lane 0 of a chunk reads that
+  //    previous position itself.
+  uint32_t len = 0;
+  if (tid < nl) {
+    s_beg[tid] = a.list_beg[(size_t)q * nl + tid];
+    len = a.list_len[(size_t)q * nl + tid];
+  }
+  const uint32_t excl = BlockExclusiveScan(len, s_part, &s_total);
+  if (tid < nl) s_off[tid] = excl;
+  if (tid == 0) s_off[nl] = s_total;
+  __syncthreads();
+  const uint32_t n = s_off[nl];
+  const uint32_t nchunks = (n + 63) >> 6;
+  constexpr uint32_t kU = 4;
+  for (uint32_t c0 = wave * kU; c0 < nchunks; c0 += (BLOCK / 64) * kU) {
+    uint32_t pos[kU], prv[kU], lst[kU];
 #pragma unroll
-    for (uint32_t t = 0; t < kLG; ++t) {
-      const uint32_t j = j0 + t;
-      beg[t] = j < nl ? a.list_beg[(size_t)q * nl + j] : 0;
-      len[t] = j < nl ? a.list_len[(size_t)q * nl + j] : 0;
-      d0[t] = j * a.shift;
-      carry[t] = 0xFFFFFFFFu;  // last bin of the list's previous chunk (none yet)
-      maxlen = max(maxlen, len[t]);
+    for (uint32_t u = 0; u < kU; ++u) {
+      const uint32_t i = ((c0 + u) << 6) + lane;
+      pos[u] = 0;
+      prv[u] = 0xFFFFFFFFu;
+      lst[u] = 0xFFFFFFFFu;
+      if (i < n) {
+        // list of entry i: first list of the chunk by binary search (uniform),
+        // then at most a few boundaries inside the chunk
+        uint32_t j = UpperIndex(s_off, nl - 1, (c0 + u) << 6);
+        while (s_off[j + 1] <= i) ++j;
+        const uint32_t r = i - s_off[j];
+        pos[u] = a.positions[s_beg[j] + r];
+        lst[u] = j;
+        if (lane == 0 && r > 0) prv[u] = a.positions[s_beg[j] + r - 1];
+      }
     }
-    for (uint32_t r0 = 0; r0 < maxlen; r0 += 64) {
-      const uint32_t r = r0 + lane;
-      uint32_t pos[kLG];
 #pragma unroll
-      for (uint32_t t = 0; t < kLG; ++t) pos[t] = r < len[t] ? a.positions[beg[t] + r] : 0u;
-#pragma unroll
-      for (uint32_t t = 0; t < kLG; ++t) {
-        const bool ok = r < len[t];
-        const uint32_t bin = ok ? (pos[t] - d0[t]) >> a.log_region : 0xFFFFFFFEu;
-        uint32_t prev = __shfl_up(bin, 1);
-        if (lane == 0) prev = carry[t];
-        carry[t] = __shfl(bin, 63);
-        if (ok && bin != prev) table.Insert(bin);
+    for (uint32_t u = 0; u < kU; ++u) {
+      const uint32_t j = lst[u];
+      const uint32_t pj = __shfl_up(j, 1), pp = __shfl_up(pos[u], 1);
+      uint32_t prev_pos = prv[u];
+      if (lane > 0 && pj == j) prev_pos = pp;
+      if (j != 0xFFFFFFFFu) {
+        const uint32_t d0 = j * a.shift;
+        const uint32_t bin = (pos[u] - d0) >> a.log_region;
+        const bool dup = prev_pos != 0xFFFFFFFFu && ((prev_pos - d0) >> a.log_region) == bin;
+        if (!dup) table.Insert(bin);
       }
     }
   }
