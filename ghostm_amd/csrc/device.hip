@@ -82,9 +82,15 @@ struct DevQuery {
   uint32_t ngroups = 0;
 };
 
+// DB residues live at seq + kDbFront, with END bytes in front of and behind
+// them, so K2 can load window residues unconditionally (the window test picks
+// END for columns outside it).
+constexpr uint32_t kDbFront = kern::kDbFrontPad, kDbBack = 65536;
+
 struct DevDb {
   DevBuf seq, kc, pos;
   uint32_t len = 0, kcl = 0, npos = 0;
+  const uint8_t *Residues() const { return seq.as<uint8_t>() + kDbFront; }
   DevBuf subj;                     // subject starts (device merge)
   uint32_t nsubj = 0;
 };
@@ -195,14 +201,18 @@ DevQuery *DeviceModule::UploadQuery(const uint8_t *seq, uint32_t nseq, uint32_t 
 DevDb *DeviceModule::UploadDb(const uint8_t *seq, uint32_t len, const uint32_t *kc, uint32_t kcl,
                               const uint32_t *pos, uint32_t npos) {
   if (!impl_) throw Error("device not bound");
+  // the kernels index 32-entry tables by residue code
+  for (uint32_t k = 0; k < len; ++k)
+    if (seq[k] >= 32) throw Error("database residue code out of range");
   DevDb *d = new DevDb();
   d->len = len;
   d->kcl = kcl;
   d->npos = npos;
-  d->seq.Reserve((size_t)len + 16);
+  d->seq.Reserve((size_t)kDbFront + len + kDbBack);
   d->kc.Reserve((size_t)kcl * 4);
   d->pos.Reserve((size_t)npos * 4 + 4);
-  if (len) HIP_CHECK(hipMemcpy(d->seq.p, seq, len, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemset(d->seq.p, (int)kern::kSeqEnd, (size_t)kDbFront + len + kDbBack));
+  if (len) HIP_CHECK(hipMemcpy(static_cast<uint8_t *>(d->seq.p) + kDbFront, seq, len, hipMemcpyHostToDevice));
   if (kcl) HIP_CHECK(hipMemcpy(d->kc.p, kc, (size_t)kcl * 4, hipMemcpyHostToDevice));
   if (npos) HIP_CHECK(hipMemcpy(d->pos.p, pos, (size_t)npos * 4, hipMemcpyHostToDevice));
   return d;
@@ -483,8 +493,9 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
   const bool gaps_ok = gap.open <= 0 && gap.ext <= 0 && -gap.open < 2000 && -gap.ext < 2000;
   const int64_t bound = (int64_t)q->L * max_abs;
   const bool allow_packed = !(force && strcmp(force, "int32") == 0);
-  const bool half = allow_packed && !(force && strcmp(force, "int16") == 0) && gaps_ok && bound < 2048;
-  const bool packed = allow_packed && gaps_ok && bound < 30000;
+  const bool half = allow_packed && !(force && strcmp(force, "int16") == 0) && gaps_ok && bound < 2048 &&
+                    base + 64 < kDbBack;
+  const bool packed = allow_packed && gaps_ok && bound < 30000 && base + 64 < kDbBack;
   const uint32_t per_block = (kern::kScoreBlock / 64) * lay.gpw * (packed ? 2 : 1);
   // tasks: runs of <= per_block consecutive candidates spanning <= Qmax queries
   std::vector<kern::ScoreTask> tasks;
@@ -526,7 +537,7 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
   a.pad = lay.Lpad - q->L;
   a.G = lay.G;
   a.gpw = lay.gpw;
-  a.db = d->seq.as<uint8_t>();
+  a.db = d->Residues();
   a.dblen = d->len;
   a.mat = I.mat_k2.as<int>();
   a.cand_qid = I.cand_qid.as<uint32_t>();
@@ -542,7 +553,7 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
   I.counters.Reserve(16);
   HIP_CHECK(hipMemsetAsync(I.counters.p, 0, 16, S(stream_)));
   a.cells = I.counters.as<unsigned long long>();
-  const size_t lds = packed ? (size_t)kern::kScoreQmax * kern::kProfRows * (lay.Lpad + 8) * 2
+  const size_t lds = packed ? (size_t)kern::kScoreQmax * kern::kProfRows16 * (lay.Lpad + 8) * 2
                             : (size_t)kern::kScoreQmax * kern::kProfRows * (lay.Lpad + 4) * 4;
   HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
   const dim3 grid((uint32_t)tasks.size()), block(kern::kScoreBlock);
@@ -670,7 +681,7 @@ void DeviceModule::MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, 
   kern::TbArgs a{};
   a.qseq = q->seq.as<uint8_t>();
   a.L = q->L;
-  a.db = d->seq.as<uint8_t>();
+  a.db = d->Residues();
   a.mat_tb = I.mat_tb.as<int>();
   a.qid = I.tb_qid.as<uint32_t>();
   a.end = I.tb_end.as<uint32_t>();
@@ -719,7 +730,7 @@ void DeviceModule::TraceBack(DevQuery *q, DevDb *d, uint32_t n, const uint32_t *
   kern::TbArgs a{};
   a.qseq = q->seq.as<uint8_t>();
   a.L = q->L;
-  a.db = d->seq.as<uint8_t>();
+  a.db = d->Residues();
   a.mat_tb = I.mat_tb.as<int>();
   a.qid = I.tb_qid.as<uint32_t>();
   a.end = I.tb_end.as<uint32_t>();

@@ -542,6 +542,8 @@ __device__ inline void WaveAddCells(unsigned long long *counter, unsigned long l
 constexpr int kScoreBlock = 256;
 constexpr int kScoreQmax = 4;
 constexpr uint32_t kProfRows = 26;
+constexpr uint32_t kProfRows16 = 32;  // packed kernels: one profile row per residue code
+constexpr uint32_t kDbFrontPad = 64;  // END bytes in front of the DB residues (device.hip)
 
 struct ScoreTask {
   unsigned long long begin;  // first candidate (global index)
@@ -770,6 +772,13 @@ template <> struct Cells<true> {
   }
 };
 
+__device__ inline uint32_t MulU24(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// 4 workgroups (16 waves) per CU: the register budget that keeps 4 waves per SIMD
 template <int S, bool HALF>
 __global__ __launch_bounds__(kScoreBlock) void k_score16(ScoreArgs a) {
   using C = Cells<HALF>;
@@ -777,14 +786,16 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16(ScoreArgs a) {
   const ScoreTask t = a.tasks[blockIdx.x];
   const uint32_t RS = a.Lpad + 8;  // 16-bit elements; 16-byte pad spreads LDS banks
 
-  const uint32_t per_slot = kProfRows * a.Lpad;
+  // per-query profiles, 32 rows (one per residue code: 0..24 the matrix, 25..31
+  // zero), so a DB code indexes its row directly
+  const uint32_t per_slot = kProfRows16 * a.Lpad;
   const uint32_t total = t.q_count * per_slot;
   for (uint32_t e = threadIdx.x; e < total; e += kScoreBlock) {
     const uint32_t slot = e / per_slot, rem = e - slot * per_slot;
     const uint32_t c = rem / a.Lpad, r = rem - c * a.Lpad;
     int v = kNeg16;
     if (r >= a.pad) v = c < 25 ? a.mat[c * 32 + a.qseq[(size_t)(t.q_first + slot) * a.L + (r - a.pad)]] : 0;
-    s_prof16[(slot * kProfRows + c) * RS + r] = C::Encode(v);
+    s_prof16[(slot * kProfRows16 + c) * RS + r] = C::Encode(v);
   }
   __syncthreads();
 
@@ -810,40 +821,48 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16(ScoreArgs a) {
     wB = a.base;
     if (offB + wB > a.dblen) wB = a.dblen - offB;
   }
-  const short *profA = s_prof16 + slotA * kProfRows * RS + i * S;
-  const short *profB = s_prof16 + slotB * kProfRows * RS + i * S;
+  // element index of profile row 0 of this lane's rows; row c is + c * RS
+  const uint32_t baseA = slotA * kProfRows16 * RS + i * S;
+  const uint32_t baseB = slotB * kProfRows16 * RS + i * S;
+  // DB residues are padded with END on both sides (kDbFrontPad in front): the
+  // column loads below need no bounds test, the window test picks END
+  const uint8_t *dbp = a.db - kDbFrontPad;
+  const uint32_t xA = offA + kDbFrontPad, xB = offB + kDbFrontPad;
   const C cell(a.open, a.ext);
 
   uint32_t H[S], E[S];
 #pragma unroll
   for (int k = 0; k < S; ++k) { H[k] = 0; E[k] = 0; }
-  uint32_t bestA = 0, bestB = 0;
-  int colA = 0, colB = 0;
-  uint32_t ncols = 0;
+  uint32_t best = 0;                     // packed best column max (16-bit patterns)
+  uint32_t col = 0;                      // packed column of the last best (>=)
+  uint32_t ncols = 0;                    // packed count of non-END columns
   uint32_t hout = 0, fout = 0, hprev = 0;
-  uint32_t prev_end = 0xFFFFFFFFu;  // the column before the first one: nothing to carry
+  uint32_t prev_end = 0xFFFFFFFFu;       // the column before the first one: nothing to carry
   int j = -(int)i;
-  uint32_t nA = kSeqEnd, nB = kSeqEnd;
-  if (j >= 0 && (uint32_t)j < wA) nA = a.db[offA + j];
-  if (j >= 0 && (uint32_t)j < wB) nB = a.db[offB + j];
+  uint32_t jj = (uint32_t)j & 0xFFFFu;
+  jj |= jj << 16;                        // packed column index (both halves)
+  // residues two deep: n* = this column's (window-tested), x* = next column's raw
+  uint32_t nA = dbp[xA + j], nB = dbp[xB + j];
+  nA = (uint32_t)j < wA ? nA : kSeqEnd;
+  nB = (uint32_t)j < wB ? nB : kSeqEnd;
+  uint32_t pxA = dbp[xA + (uint32_t)(j + 1)], pxB = dbp[xB + (uint32_t)(j + 1)];
   const uint32_t steps = a.base + a.G - 1;
-  for (uint32_t step = 0; step < steps; ++step, ++j) {
+  for (uint32_t step = 0; step < steps; ++step, ++j, jj += 0x00010001u) {
     uint32_t hin = ShiftUp(hout), fin = ShiftUp(fout);
     if (i == 0) { hin = 0; fin = 0; }
     const uint32_t diag0 = hprev;
     hprev = hin;
     const uint32_t rA = nA, rB = nB;
-    nA = kSeqEnd;
-    nB = kSeqEnd;
-    if (j + 1 >= 0 && (uint32_t)(j + 1) < wA) nA = a.db[offA + j + 1];
-    if (j + 1 >= 0 && (uint32_t)(j + 1) < wB) nB = a.db[offB + j + 1];
+    nA = (uint32_t)(j + 1) < wA ? pxA : kSeqEnd;
+    nB = (uint32_t)(j + 1) < wB ? pxB : kSeqEnd;
+    pxA = dbp[xA + (uint32_t)(j + 2)];
+    pxB = dbp[xB + (uint32_t)(j + 2)];
     // inactive columns (fill, drain, beyond the window) behave as END
-    const bool endA = rA == kSeqEnd, endB = rB == kSeqEnd;
-    const uint32_t end = (endA ? 0x0000FFFFu : 0u) | (endB ? 0xFFFF0000u : 0u);
+    const uint32_t end = (rA == kSeqEnd ? 0x0000FFFFu : 0u) | (rB == kSeqEnd ? 0xFFFF0000u : 0u);
     const typename C::Step st = cell.At(end, prev_end);
     prev_end = end;
-    const short *pA = profA + (rA < 25 ? rA : 25u) * RS;
-    const short *pB = profB + (rB < 25 ? rB : 25u) * RS;
+    const short *pA = s_prof16 + (baseA + MulU24(rA, RS));
+    const short *pB = s_prof16 + (baseB + MulU24(rB, RS));
     uint32_t diag = diag0, F = fin, cm = 0;
 #pragma unroll
     for (int k = 0; k < S; k += 8) {
@@ -870,17 +889,17 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16(ScoreArgs a) {
     }
     hout = H[S - 1];
     fout = F;
-    const uint32_t cmA = cm & 0xFFFFu, cmB = cm >> 16;
-    if (!endA) {
-      if (cmA >= bestA) { bestA = cmA; colA = j; }
-      ++ncols;
-    }
-    if (!endB) {
-      if (cmB >= bestB) { bestB = cmB; colB = j; }
-      ++ncols;
+    {
+      const uint32_t cmA = cm & 0xFFFFu, cmB = cm >> 16;
+      uint32_t bA = best & 0xFFFFu, bB = best >> 16, oA = col & 0xFFFFu, oB = col >> 16;
+      if (!(end & 1u)) { if (cmA >= bA) { bA = cmA; oA = (uint32_t)j; } ncols += 1; }
+      if (!(end >> 31)) { if (cmB >= bB) { bB = cmB; oB = (uint32_t)j; } ncols += 0x10000u; }
+      best = bA | (bB << 16);
+      col = oA | (oB << 16);
     }
   }
-  int BA = C::Decode(bestA), CA = colA, BB = C::Decode(bestB), CB = colB;
+  int BA = C::Decode(best & 0xFFFFu), CA = (int)(col & 0xFFFFu);
+  int BB = C::Decode(best >> 16), CB = (int)(col >> 16);
   for (uint32_t k = 1; k < a.G; ++k) {
     const int src = (int)(g * a.G + k);
     const int oba = __shfl(BA, src), oca = __shfl(CA, src);
@@ -898,7 +917,8 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16(ScoreArgs a) {
       a.end_out[cB - a.out_base] = offB + (uint32_t)CB;
     }
   }
-  WaveAddCells(a.cells, (in_group && i == 0) ? (unsigned long long)ncols * a.L : 0ull);
+  WaveAddCells(a.cells, (in_group && i == 0) ? (unsigned long long)((ncols & 0xFFFFu) + (ncols >> 16)) * a.L
+                                             : 0ull);
 }
 
 // ------------------------------------------------------------------ K3 traceback
