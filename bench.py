@@ -78,7 +78,9 @@ def cpu_baseline(root: str, nsample: int, db_res: int, first: int) -> dict:
 
 
 def _device() -> int:
-    return int(os.environ.get("LOCAL_RANK", "0"))
+    # GHOSTM_BENCH_DEVICE pins every rank to one device (rehearsing the
+    # multi-rank path on a one-GPU machine)
+    return int(os.environ.get("GHOSTM_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0")))
 
 
 def load_pmc_traffic() -> dict | None:
@@ -109,7 +111,11 @@ def main() -> None:
         import torch.distributed as dist
 
         torch.cuda.set_device(_device())
-        dist.init_process_group("nccl")
+        # RCCL ("nccl") over xGMI; GHOSTM_BENCH_BACKEND=gloo rehearses the same
+        # calls on a one-GPU machine (RCCL refuses two ranks on one device)
+        backend = os.environ.get("GHOSTM_BENCH_BACKEND", "nccl")
+        dist.init_process_group(backend)
+        coll_dev = "cuda" if backend == "nccl" else "cpu"
     from ghostm_amd.aligner import Session
 
     workdir = args.workdir or tempfile.mkdtemp(prefix=f"ghostm_bench_r{rank}_")
@@ -122,11 +128,12 @@ def main() -> None:
     def step():
         sess.run()
         if dist is not None:
-            from ghostm_amd.shard import gather_hits
+            from ghostm_amd.aligner import HIT_DTYPE
+            from ghostm_amd.shard import gather_device_records
 
-            merged = gather_hits(sess.hits(), dist, "cuda")
+            merged = gather_device_records(sess.device_hits().to(coll_dev), dist, HIT_DTYPE.itemsize)
             if rank == 0:
-                step.gathered = sum(len(m) for m in merged)
+                step.gathered = sum(m.numel() for m in merged) // HIT_DTYPE.itemsize
     step.gathered = 0
 
     for _ in range(args.warmup):
@@ -154,10 +161,10 @@ def main() -> None:
     if dist is not None:
         import torch
 
-        e = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        e = torch.tensor([elapsed], device=coll_dev, dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
-        res = torch.tensor([st_acc["query_residues"]], device="cuda", dtype=torch.float64)
+        res = torch.tensor([st_acc["query_residues"]], device=coll_dev, dtype=torch.float64)
         dist.all_reduce(res)
         total_res = float(res.item())
     else:

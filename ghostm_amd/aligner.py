@@ -80,6 +80,23 @@ class Session:
             lib.GhostmSessionHits(self._h, out.ctypes.data_as(ctypes.POINTER(native.GhostmHit)), n)
         return out
 
+    def device_hits(self, device="cuda"):
+        """The hit records as a torch uint8 tensor on this session's GPU (32 bytes
+        per record, HIT_DTYPE layout), copied device-to-device — the payload of
+        the multi-GPU gather."""
+        import torch
+
+        lib = native.load()
+        n = lib.GhostmSessionDeviceHits(self._h, None, 0)
+        if n == ctypes.c_size_t(-1).value:
+            raise GhostmError(native.last_error())
+        out = torch.empty(max(n, 1) * HIT_DTYPE.itemsize, dtype=torch.uint8, device=device)
+        if n:
+            torch.cuda.synchronize(out.device)
+            if lib.GhostmSessionDeviceHits(self._h, ctypes.c_void_p(out.data_ptr()), n) != n:
+                raise GhostmError(native.last_error())
+        return out[: n * HIT_DTYPE.itemsize]
+
     def stats(self) -> dict:
         st = native.GhostmStats()
         native.load().GhostmSessionStats(self._h, ctypes.byref(st))

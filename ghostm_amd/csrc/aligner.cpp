@@ -403,6 +403,7 @@ void Session::DeviceMergePath(QueryData &q, DbData &d, const std::vector<uint32_
     }
     stats_.seconds_merge += NowSeconds() - t0;
     for (uint32_t c : *sel_counts) stats_.tracebacks += c;
+    if (c1 > c0) dev.AppendRecords(q.dev, g0, *sel_counts, cap, q.global_base, d.global_base);
     Part *part = NewPart();
     const QueryData *qp = &q;
     formatter_->Submit([this, qp, g0, sel_counts, sel_hits, cap, part] {
@@ -442,6 +443,7 @@ void Session::RunQueryChunk(QueryData &q) {
       return;
     }
     if (!results) results.reset(new Results(q.chunk.nseq));
+    records_on_device_ = false;  // host merge: records are uploaded on demand
     for (const Batch &b : batches) {
       const uint64_t c0 = offsets[b.q0];
       const uint64_t c1 = b.q1 < counts.size() ? offsets[b.q1] : total;
@@ -680,6 +682,8 @@ void Session::Run() {
   hits_.clear();
   hits_valid_ = false;
   Format();  // built here, before any formatting task can need it
+  dev.ResetRecords();
+  records_on_device_ = true;
   const double t0 = NowSeconds();
   for (QueryData &q : queries_) {
     RunQueryChunk(q);
@@ -727,6 +731,18 @@ const std::vector<GhostmHit> &Session::Hits() {
     hits_valid_ = true;
   }
   return hits_;
+}
+
+size_t Session::DeviceHits(void *dst, size_t cap) {
+  DeviceModule &dev = DeviceModule::Get();
+  if (!records_on_device_) {
+    const std::vector<GhostmHit> &h = Hits();
+    dev.UploadRecords(h.data(), h.size());
+    records_on_device_ = true;
+  }
+  const size_t n = (size_t)dev.RecordCount();
+  if (dst && cap) dev.CopyRecords(dst, std::min(n, cap));
+  return n;
 }
 
 void Session::WriteOutputFile() {

@@ -99,6 +99,9 @@ class Session {
   const std::string &Output();         // text of the last run (joined on first use)
   void WriteOutputFile();
   const std::vector<GhostmHit> &Hits();
+  // Hit records of the last run in device memory (this session's GPU): copies
+  // min(n, cap) records to dst_device; returns n.
+  size_t DeviceHits(void *dst_device, size_t cap);
   const GhostmStats &Stats() const { return stats_; }
 
  private:
@@ -148,6 +151,7 @@ class Session {
   bool joined_valid_ = false;
   std::vector<GhostmHit> hits_;
   bool hits_valid_ = false;
+  bool records_on_device_ = false;
   GhostmStats stats_{};
   unsigned threads_ = 1;
   std::unique_ptr<TaskQueue> formatter_;

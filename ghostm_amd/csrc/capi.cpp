@@ -66,6 +66,16 @@ size_t GhostmSessionHits(void *s, GhostmHit *hits, size_t cap) {
   return n;
 }
 
+size_t GhostmSessionDeviceHits(void *s, void *dst_device, size_t cap) {
+  try {
+    if (!s) throw Error("null session");
+    return static_cast<Session *>(s)->DeviceHits(dst_device, cap);
+  } catch (std::exception &e) {
+    SetLastErrorMessage(e.what());
+    return (size_t)-1;
+  }
+}
+
 int GhostmSessionStats(void *s, GhostmStats *stats) {
   if (!s || !stats) return 1;
   *stats = static_cast<Session *>(s)->Stats();

@@ -98,6 +98,16 @@ class DeviceModule {
                    uint32_t tb_base, int open, int ext, std::vector<uint32_t> *counts,
                    std::vector<SelectedHit> *hits);
 
+  // Device-resident hit records of the current run (GhostmHit layout, 32 B),
+  // for the multi-GPU gather. AppendRecords turns the last MergeSelect's hits
+  // (groups [g0, g0 + counts.size())) into records at the end of the array.
+  void ResetRecords();
+  void AppendRecords(DevQuery *q, uint32_t g0, const std::vector<uint32_t> &counts, uint32_t cap,
+                     uint32_t q_base, uint32_t d_base);
+  void UploadRecords(const void *records, uint64_t n);  // host records (other paths)
+  uint64_t RecordCount() const { return records_; }
+  void CopyRecords(void *dst_device, uint64_t n);         // device-to-device, synchronous
+
   // K3 on n hits (query id, absolute db end).
   void TraceBack(DevQuery *q, DevDb *d, uint32_t n, const uint32_t *qid, const uint32_t *db_end,
                  uint32_t base_search_length, int open, int ext, uint32_t *db_start,
@@ -113,6 +123,7 @@ class DeviceModule {
   int device_ = -1;
   void *stream_ = nullptr;
   DeviceTimes times_;
+  uint64_t records_ = 0;
   struct Impl;
   Impl *impl_ = nullptr;
   friend struct DeviceModuleAccess;

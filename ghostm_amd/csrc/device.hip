@@ -101,6 +101,8 @@ struct DeviceModule::Impl {
   // K1 work
   DevBuf counts, nelem, slots, offsets, qlist, gbuf, gbuf_off, list_beg, list_len;
   DevBuf cand_start, cand_qid;
+  DevBuf records, rec_prefix;    // hit records of the run (HitRecord32)
+  std::vector<uint32_t> h_rec_prefix;
   uint64_t ncand = 0;
   // K2 work
   DevBuf tasks, score_out, end_out;
@@ -713,6 +715,64 @@ void DeviceModule::MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, 
   HIP_CHECK(hipStreamSynchronize(S(stream_)));
   times_.traceback += ElapsedMs(I.ev0, I.ev1) * 1e-3;
   times_.traceback_cells += cells;
+}
+
+void DeviceModule::ResetRecords() { records_ = 0; }
+
+static void GrowRecords(DevBuf &buf, uint64_t records, uint64_t want, hipStream_t st) {
+  const size_t need = (size_t)want * sizeof(kern::HitRecord32);
+  if (need <= buf.bytes) return;
+  DevBuf bigger;
+  bigger.Reserve(std::max(need, buf.bytes * 2));
+  if (records) HIP_CHECK(hipMemcpyAsync(bigger.p, buf.p, (size_t)records * sizeof(kern::HitRecord32),
+                                        hipMemcpyDeviceToDevice, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+  buf.Release();
+  buf = bigger;
+  bigger.p = nullptr;
+  bigger.bytes = 0;
+}
+
+void DeviceModule::AppendRecords(DevQuery *q, uint32_t g0, const std::vector<uint32_t> &counts, uint32_t cap,
+                                 uint32_t q_base, uint32_t d_base) {
+  Impl &I = *impl_;
+  const uint32_t ng = (uint32_t)counts.size();
+  if (ng == 0) return;
+  std::vector<uint32_t> &prefix = I.h_rec_prefix;  // kept alive for the async copy
+  prefix.resize(ng);
+  uint64_t total = 0;
+  for (uint32_t g = 0; g < ng; ++g) {
+    prefix[g] = (uint32_t)total;
+    total += counts[g];
+  }
+  if (total == 0) return;
+  GrowRecords(I.records, records_, records_ + total, S(stream_));
+  I.rec_prefix.Reserve((size_t)ng * 4);
+  HIP_CHECK(hipMemcpyAsync(I.rec_prefix.p, prefix.data(), (size_t)ng * 4, hipMemcpyHostToDevice, S(stream_)));
+  hipLaunchKernelGGL(kern::k_records, dim3((ng + 255) / 256), dim3(256), 0, S(stream_), I.sel_count.as<uint32_t>(),
+                     I.slot_hits.as<kern::SlotHit>(), I.rec_prefix.as<uint32_t>(),
+                     q->group_last.as<uint32_t>() + g0, ng, cap, q_base, d_base,
+                     I.records.as<kern::HitRecord32>() + records_);
+  HIP_CHECK(hipGetLastError());
+  records_ += total;
+}
+
+void DeviceModule::UploadRecords(const void *recs, uint64_t n) {
+  Impl &I = *impl_;
+  records_ = 0;
+  if (n == 0) return;
+  GrowRecords(I.records, 0, n, S(stream_));
+  HIP_CHECK(hipMemcpy(I.records.p, recs, (size_t)n * sizeof(kern::HitRecord32), hipMemcpyHostToDevice));
+  records_ = n;
+}
+
+void DeviceModule::CopyRecords(void *dst, uint64_t n) {
+  Impl &I = *impl_;
+  n = std::min(n, records_);
+  if (n == 0) return;
+  HIP_CHECK(hipMemcpyAsync(dst, I.records.p, (size_t)n * sizeof(kern::HitRecord32), hipMemcpyDeviceToDevice,
+                           S(stream_)));
+  HIP_CHECK(hipStreamSynchronize(S(stream_)));
 }
 
 void DeviceModule::TraceBack(DevQuery *q, DevDb *d, uint32_t n, const uint32_t *qid,

@@ -1258,5 +1258,27 @@ __global__ void k_finalize(const uint32_t *sel_count, const uint32_t *sel_cand,
   out[s] = SlotHit{sid, score[c], tb_start[s] - pos, end[c] - pos, tb_ml[s]};
 }
 
+// The gathered hit record (include/ghostm_hip.h GhostmHit), written on the
+// device for the multi-GPU gather: one thread per name group, its hits at the
+// group's prefix offset; seq_id = match / len in float as aligner.cpp:945.
+struct HitRecord32 {
+  uint32_t query_id, db_id, score, db_start, db_end, aln_len, aln_match;
+  float seq_id;
+};
+
+__global__ void k_records(const uint32_t *sel_count, const SlotHit *slots, const uint32_t *prefix,
+                          const uint32_t *group_last, uint32_t ng, uint32_t cap, uint32_t q_base,
+                          uint32_t d_base, HitRecord32 *out) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ng) return;
+  const uint32_t n = sel_count[g], at = prefix[g], qid = q_base + group_last[g];
+  for (uint32_t k = 0; k < n; ++k) {
+    const SlotHit h = slots[(size_t)g * cap + k];
+    const uint32_t len = h.ml >> 8, match = h.ml & 0xFFu;
+    out[at + k] = HitRecord32{qid, d_base + h.sid, h.score, h.start, h.end, len, match,
+                              (float)match / (float)len};
+  }
+}
+
 }  // namespace kern
 }  // namespace ghostm

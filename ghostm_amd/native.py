@@ -85,6 +85,7 @@ SIGNATURES = {
     "GhostmSessionOutput": (c_size_t, [c_void_p, c_char_p, c_size_t]),
     "GhostmSessionWrite": (c_int, [c_void_p]),
     "GhostmSessionHits": (c_size_t, [c_void_p, POINTER(GhostmHit), c_size_t]),
+    "GhostmSessionDeviceHits": (c_size_t, [c_void_p, c_void_p, c_size_t]),
     "GhostmSessionStats": (c_int, [c_void_p, POINTER(GhostmStats)]),
     "GhostmSessionDestroy": (None, [c_void_p]),
     "GhostmAlignMain": (c_int, [c_int, POINTER(c_char_p)]),

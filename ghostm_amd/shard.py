@@ -43,6 +43,29 @@ def balanced_cuts(weights: Sequence[int], names: Sequence[str], world: int) -> l
     return cuts
 
 
+def gather_device_records(payload, dist, itemsize: int):
+    """One gather of every rank's hit records, already on its GPU as a uint8
+    tensor (Session.device_hits), to rank 0 over RCCL — no host copies on any
+    rank. Returns rank 0's list of per-rank uint8 tensors (device), None elsewhere."""
+    import torch
+
+    world = dist.get_world_size()
+    rank = dist.get_rank()
+    n = torch.tensor([payload.numel()], device=payload.device, dtype=torch.int64)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n)
+    cap = max(int(s.item()) for s in sizes)
+    buf = payload
+    if payload.numel() != cap or cap == 0:
+        buf = torch.zeros(max(cap, itemsize), dtype=torch.uint8, device=payload.device)
+        buf[: payload.numel()] = payload
+    gathered = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+    dist.gather(buf, gathered, dst=0)
+    if rank != 0:
+        return None
+    return [g[: int(s.item())] for g, s in zip(gathered, sizes)]
+
+
 def gather_hits(hits: np.ndarray, dist, device) -> list[np.ndarray] | None:
     """Gather every rank's hit records (a structured array of any dtype) to rank 0.
     Returns the per-rank arrays in rank order on rank 0, None elsewhere. Sizes

@@ -163,6 +163,12 @@ int GhostmSessionWrite(void *session);
 /* Hit records of the last run in output order; same NULL/cap convention. */
 size_t GhostmSessionHits(void *session, GhostmHit *hits, size_t cap);
 
+/* The same records resident on the session's GPU, for a device-to-device
+ * gather across ranks: copies min(n, cap) records to dst_device
+ * (device memory on the session's GPU; NULL only counts) and returns n, or
+ * (size_t)-1 on error. */
+size_t GhostmSessionDeviceHits(void *session, void *dst_device, size_t cap);
+
 int GhostmSessionStats(void *session, GhostmStats *stats);
 
 void GhostmSessionDestroy(void *session);

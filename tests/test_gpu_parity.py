@@ -229,3 +229,20 @@ def test_reference_driver_on_this_plugin(ds, var, opts, env, dataset, golden, tm
     out = str(tmp_path / "ref_gpu.out")
     cases.run_aln(cases.REF, d, list(opts) + ["-D", "0"], env, out)
     assert cases.sha256(out) == golden["aln"][f"{ds}/{var}"]["sha256"]
+
+
+@pytest.mark.parametrize("ds,opts", [("syn_small", []), ("syn_dna", []), ("syn_chunks", [])])
+def test_device_records_equal_host_records(ds, opts, dataset, tmp_path):
+    """The device-resident hit records (the multi-GPU gather payload) are the
+    host records byte for byte: built per segment on the device (device merge,
+    syn_small / syn_dna) or uploaded from the host merge (syn_chunks)."""
+    d = dataset(ds)
+    with Session(["-i", f"{d}/q", "-d", f"{d}/db", "-o", str(tmp_path / "x"), "-D", "0"] + opts) as s:
+        s.run()
+        host = s.hits()
+        dev = s.device_hits().cpu().numpy()
+        s.run()  # records are rebuilt per run, not appended
+        dev2 = s.device_hits().cpu().numpy()
+    assert len(host) > 0
+    assert dev.tobytes() == host.tobytes()
+    assert dev2.tobytes() == host.tobytes()

@@ -40,7 +40,8 @@ WORKER = textwrap.dedent("""
     import torch.distributed as dist
     sys.path.insert(0, {repo!r})
     from ghostm_amd.aligner import HIT_DTYPE
-    from ghostm_amd.shard import gather_hits
+    import torch
+    from ghostm_amd.shard import gather_device_records, gather_hits
     rank, world = int(sys.argv[1]), int(sys.argv[2])
     dist.init_process_group("gloo", rank=rank, world_size=world)
     n = [3, 0, 5][rank]  # rank 1 holds no hits
@@ -48,9 +49,13 @@ WORKER = textwrap.dedent("""
     h["query_id"] = rank * 100 + np.arange(n)
     h["seq_id"] = 0.25 * rank
     out = gather_hits(h, dist, "cpu")
+    # the device-record form (uint8 payload tensors; CPU tensors over gloo here)
+    dev = gather_device_records(torch.from_numpy(h.view(np.uint8).copy()), dist, HIT_DTYPE.itemsize)
     if rank == 0:
         np.save(sys.argv[3], np.concatenate(out))
         assert [len(x) for x in out] == [3, 0, 5][:world]
+        flat = np.concatenate([t.numpy() for t in dev]).view(HIT_DTYPE)
+        assert flat.tobytes() == np.concatenate(out).tobytes()
     dist.barrier()
     dist.destroy_process_group()
 """)
