@@ -13,7 +13,8 @@ from ctypes import POINTER, c_char_p, c_float, c_int, c_size_t, c_uint32, c_uint
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libghostm_hip.so")
+# GHOSTM_LIB_PATH selects another build of the same library (A/B timing runs)
+LIB_PATH = os.environ.get("GHOSTM_LIB_PATH") or os.path.join(PKG_DIR, "lib", "libghostm_hip.so")
 BIN_PATH = os.path.join(PKG_DIR, "bin", "ghostm")
 HEADER_PATH = os.path.join(REPO_DIR, "include", "ghostm_hip.h")
 
