@@ -97,7 +97,7 @@ struct DevDb {
 
 struct DeviceModule::Impl {
   int h_matrix[32 * 32] = {0};
-  DevBuf mat_k2, mat_tb, mat_tbk;
+  DevBuf mat_k2, mat_tb, mat_tbk;  // mat_tbk: two 32x32 key tables (MLW 16, 17)
   // K1 work
   DevBuf counts, nelem, slots, offsets, qlist, gbuf, gbuf_off, list_beg, list_len;
   DevBuf cand_start, cand_qid;
@@ -169,13 +169,19 @@ void DeviceModule::SetMatrix(const int *m) {
                                                 : (int)(((unsigned)v << 16) | (unsigned)inc);
     }
   }
-  // K3 key table: (score << 18) | (2 << 16) | (0x80 | eq); padding rows score far
-  // below any reachable h (k_traceback_key)
-  int tbk[32 * 32];
-  for (int c = 0; c < 32; ++c) {
-    for (int q = 0; q < 32; ++q) {
-      const int v = q == (int)kern::kPadCode ? -4096 : std::max(-4096, std::min(4095, m[c * 32 + q]));
-      tbk[c * 32 + q] = (int)(((uint32_t)v << 18) | (2u << 16) | 0x80u | (c == q ? 1u : 0u));
+  // K3 key tables (k_traceback_key): (score << (MLW+2)) | (2 << MLW) | (0x80 | eq)
+  // for MLW = 16 and 17; padding rows score far below any reachable h
+  // h field: 14 bits signed (MLW 16) or 13 (MLW 17); the padding score is the
+  // field minimum, below -hmax for every launch LaunchTraceback allows
+  int tbk[2][32 * 32];
+  for (int w = 0; w < 2; ++w) {
+    const int mlw = 16 + w, lim = w ? 4095 : 8191;
+    for (int c = 0; c < 32; ++c) {
+      for (int q = 0; q < 32; ++q) {
+        const int v = q == (int)kern::kPadCode ? -lim - 1 : std::max(-lim, std::min(lim, m[c * 32 + q]));
+        tbk[w][c * 32 + q] =
+            (int)(((uint32_t)v << (mlw + 2)) | (2u << mlw) | 0x80u | (c == q ? 1u : 0u));
+      }
     }
   }
   impl_->mat_k2.Reserve(sizeof(k2));
@@ -605,27 +611,29 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, uint32_t rows, uint32_t n) {
   a.gpw = lay.gpw;
   int max_abs = 0;
   for (int v : I.h_matrix) max_abs = std::max(max_abs, v < 0 ? -v : v);
+  // path length <= rows + columns; ml = len << 7 | matches (matches <= L <= 127)
   const char *force = getenv("GHOSTM_K3");
-  const bool key = !(force && strcmp(force, "int32") == 0) && a.L <= 127 && lay.Lpad + a.base < 500 &&
-                   (int64_t)a.L * max_abs < 4000 && a.open <= 0 && a.ext <= 0 && -a.open < 4000 &&
-                   -a.ext < 4000;
-  if (key) a.mat_tb = I.mat_tbk.as<int>();
+  const bool allow = !(force && strcmp(force, "int32") == 0) && a.L <= 127 && a.open <= 0 && a.ext <= 0;
+  const uint64_t span = (uint64_t)lay.Lpad + a.base;
+  const int64_t hmax = (int64_t)a.L * max_abs;
+  // h, E, F stay in [open + ext, hmax]; the field must hold that and the padding
+  // rows' h + pad must stay negative
+  const bool key16 = allow && span < 500 && hmax < 8000 && -a.open < 4000 && -a.ext < 4000;
+  const bool key17 = !key16 && allow && span < 1000 && hmax < 4000 && -a.open < 2000 && -a.ext < 2000;
+  const bool key = key16 || key17;
+  if (key) a.mat_tb = I.mat_tbk.as<int>() + (key17 ? 32 * 32 : 0);
   const uint32_t per_block = (kern::kTbBlock / 64) * lay.gpw;
   const dim3 grid((n + per_block - 1) / per_block), block(kern::kTbBlock);
+#define GHOSTM_TB(SS)                                                                        \
+  if (key16) hipLaunchKernelGGL((kern::k_traceback_key<SS, 16>), grid, block, 0, S(stream_), a); \
+  else if (key17) hipLaunchKernelGGL((kern::k_traceback_key<SS, 17>), grid, block, 0, S(stream_), a); \
+  else hipLaunchKernelGGL(kern::k_traceback<SS>, grid, block, 0, S(stream_), a);
   switch (lay.S) {
-    case 32:
-      if (key) hipLaunchKernelGGL(kern::k_traceback_key<32>, grid, block, 0, S(stream_), a);
-      else hipLaunchKernelGGL(kern::k_traceback<32>, grid, block, 0, S(stream_), a);
-      break;
-    case 16:
-      if (key) hipLaunchKernelGGL(kern::k_traceback_key<16>, grid, block, 0, S(stream_), a);
-      else hipLaunchKernelGGL(kern::k_traceback<16>, grid, block, 0, S(stream_), a);
-      break;
-    default:
-      if (key) hipLaunchKernelGGL(kern::k_traceback_key<8>, grid, block, 0, S(stream_), a);
-      else hipLaunchKernelGGL(kern::k_traceback<8>, grid, block, 0, S(stream_), a);
-      break;
+    case 32: GHOSTM_TB(32); break;
+    case 16: GHOSTM_TB(16); break;
+    default: GHOSTM_TB(8); break;
   }
+#undef GHOSTM_TB
   HIP_CHECK(hipGetLastError());
   times_.traceback_launches += 1;
   times_.traceback_launches_key += key ? 1 : 0;

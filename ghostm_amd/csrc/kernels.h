@@ -1055,13 +1055,21 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback(TbArgs a) {
 // quirk), spliced in with one v_bfi. Per cell: table lookup, ~14 integer ops
 // and the strict first-maximum update. Used when len < 511, L <= 127 and every
 // |h| < 8192; k_traceback above covers the rest.
-constexpr uint32_t kKeyLow = (1u << 18) - 1;  // prio + ml bits
-constexpr uint32_t kKeyPrio = 3u << 16;
+// Key layout for an ml field of MLW bits (ml = len << 7 | matches): prio at
+// bits MLW..MLW+1, h from bit MLW+2 up (signed). MLW = 16 (len < 512, |h| < 8192)
+// or 17 (len < 1024, |h| < 4096, wide bands).
+template <int MLW> struct KeyLayout {
+  static constexpr int kHS = MLW + 2;
+  static constexpr uint32_t kLow = (1u << kHS) - 1;  // prio + ml bits
+  static constexpr uint32_t kPrio = 3u << MLW;
+  static constexpr uint32_t kMl = (1u << MLW) - 1;
+};
 
 __device__ inline int ShiftUpI(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xF, 0xF, false); }
 
-template <int S>
+template <int S, int MLW>
 __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
+  using KL = KeyLayout<MLW>;
   __shared__ int s_key[32 * 32];
   for (uint32_t e = threadIdx.x; e < 32 * 32; e += kTbBlock) s_key[e] = a.mat_tb[e];
   __syncthreads();
@@ -1095,11 +1103,11 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
   int kout = 0, kfout = 0, kprev = 0;
   bool done = false;
   uint32_t ncols = 0;
-  const int OPENK = (int)(((uint32_t)a.open << 18) | (1u << 16) | 0x80u);  // E: prio 1, len + 1
-  const int OPENKF = (int)(((uint32_t)a.open << 18) | 0x80u);              // F: prio 0, len + 1
-  const int EXTK = (int)((uint32_t)a.ext << 18);
-  const int KZ = (int)(3u << 16);
-  const uint32_t HIGH = ~kKeyLow;
+  const int OPENK = (int)(((uint32_t)a.open << KL::kHS) | (1u << MLW) | 0x80u);  // E: prio 1, len + 1
+  const int OPENKF = (int)(((uint32_t)a.open << KL::kHS) | 0x80u);              // F: prio 0, len + 1
+  const int EXTK = (int)((uint32_t)a.ext << KL::kHS);
+  const int KZ = (int)(3u << MLW);
+  const uint32_t HIGH = ~KL::kLow;
   int j = -(int)i;
   const uint32_t steps = a.base + a.G - 1;
   for (uint32_t step = 0; step < steps; ++step, ++j) {
@@ -1131,16 +1139,16 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
           const int u = k + v;
           const int k1 = max(ks[v], KZ);
           const int A = K[u] + OPENK;
-          const int B = (int)((((uint32_t)(KE[u] + EXTK)) & HIGH) | ((uint32_t)A & kKeyLow));
+          const int B = (int)((((uint32_t)(KE[u] + EXTK)) & HIGH) | ((uint32_t)A & KL::kLow));
           KE[u] = max(A, B);
           const int AF = kup + OPENKF;
-          const int BF = (int)((((uint32_t)(KF + EXTK)) & HIGH) | ((uint32_t)AF & kKeyLow));
+          const int BF = (int)((((uint32_t)(KF + EXTK)) & HIGH) | ((uint32_t)AF & KL::kLow));
           KF = max(AF, BF);
-          const int kc = (int)((uint32_t)max(max(k1, KE[u]), KF) & ~kKeyPrio);
+          const int kc = (int)((uint32_t)max(max(k1, KE[u]), KF) & ~KL::kPrio);
           K[u] = kc;
           kup = kc;
-          // strict > on h: the upper words are h << 2 (prio cleared)
-          if ((kc >> 16) > (bestK >> 16)) { bestK = kc; best_col = j; }
+          // strict > on h: above the ml field sit h << 2 and the cleared prio
+          if ((kc >> MLW) > (bestK >> MLW)) { bestK = kc; best_col = j; }
         }
       }
       kout = K[S - 1];
@@ -1152,12 +1160,12 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
     }
   }
   // first cell (column-major, rows in processing order) reaching the maximum
-  int B = bestK >> 18, C = best_col, ML = bestK & 0xFFFF;
+  int B = bestK >> KL::kHS, C = best_col, ML = (int)((uint32_t)bestK & KL::kMl);
   for (uint32_t k = 1; k < a.G; ++k) {
     const int src = (int)(g * a.G + k);
     const int ok = __shfl(bestK, src), oc = __shfl(best_col, src);
-    const int ob = ok >> 18;
-    if (ob > B || (ob == B && ob > 0 && oc < C)) { B = ob; C = oc; ML = ok & 0xFFFF; }
+    const int ob = ok >> KL::kHS;
+    if (ob > B || (ob == B && ob > 0 && oc < C)) { B = ob; C = oc; ML = (int)((uint32_t)ok & KL::kMl); }
   }
   if (valid && i == 0) {
     a.out_start[hit] = p0 - (uint32_t)C;

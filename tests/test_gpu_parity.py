@@ -246,3 +246,14 @@ def test_device_records_equal_host_records(ds, opts, dataset, tmp_path):
     assert len(host) > 0
     assert dev.tobytes() == host.tobytes()
     assert dev2.tobytes() == host.tobytes()
+
+
+def test_wide_band_traceback_uses_key_kernel(dataset, golden, tmp_path):
+    """-r 64 (cfg 5 style: PAM250, traceback window L + 2e*2*64 = 639 columns)
+    runs the 17-bit-ml key traceback and still reproduces the golden output."""
+    d = dataset("syn_small")
+    opts = ["-r", "64", "-M", cases.PAM250, "-y", "2"]
+    text, st = _gpu_text(d, opts, {}, str(tmp_path / "g.out"))
+    (tmp_path / "g.out").write_bytes(text)
+    assert cases.sha256(str(tmp_path / "g.out")) == golden["aln"]["syn_small/r64_pam250"]["sha256"]
+    assert st["traceback_launches_key"] == st["traceback_launches"] > 0
