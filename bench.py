@@ -32,6 +32,18 @@ PEAK_HBM_GBS = 8000.0   # HBM3E spec
 SCORE_OPS_PER_CELL = 10  # Gotoh cell: add, max3 (H), add (open), add+max (E), add+max (F), max (colmax)
 
 
+PAM250 = os.path.join(REPO, "tests", "golden", "matrices", "PAM250")
+# BASELINE.json configs: synthetic data, splitmix64 seeds 3/4/5
+PRESETS = {
+    "cfg4": {"queries": 1_000_000, "db": 10_000_000, "seed": 4, "aln": [],
+             "workload": "cfg4: synthetic 1M queries (avg 300 aa requested, L=127) x 10M-residue DB, per rank"},
+    "cfg3": {"queries": 100_000, "db": 5_000_000, "seed": 3, "aln": [],
+             "workload": "cfg3: synthetic 100k queries (L=127) x 5M-residue DB, per rank"},
+    "cfg5": {"queries": 100_000, "db": 5_000_000, "seed": 5, "aln": ["-r", "64", "-M", PAM250, "-y", "2"],
+             "workload": "cfg5: wide band -r 64, PAM250 11/1, -y 2; synthetic 100k queries x 5M-residue DB"},
+}
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -48,7 +60,8 @@ def make_data(root: str, nq: int, db_res: int, first: int, seed: int = 4) -> Non
     os.remove(f"{root}/q.fa")
 
 
-def cpu_baseline(root: str, nsample: int, db_res: int, first: int) -> dict:
+def cpu_baseline(root: str, nsample: int, db_res: int, first: int, seed: int = 4,
+                 aln_args: list | None = None) -> dict:
     """The reference's own CPU path (oracle/_ref/ghostm_ref: GHOSTM's aligner.cpp
     compiled from the reference sources, run without -D) on the first `nsample`
     queries of this rank's workload against the same DB, single-threaded as the
@@ -63,16 +76,17 @@ def cpu_baseline(root: str, nsample: int, db_res: int, first: int) -> dict:
     sub = os.path.join(root, "sample")
     os.makedirs(sub, exist_ok=True)
     subprocess.run([ghostm, "synth", "-q", f"{sub}/q.fa", "-n", str(nsample), "-N", str(db_res),
-                    "-s", "4", "-f", str(first)], check=True, capture_output=True)
+                    "-s", str(seed), "-f", str(first)], check=True, capture_output=True)
     subprocess.run([ghostm, "qry", "-i", f"{sub}/q.fa", "-o", f"{sub}/q", "-l", "300"], check=True,
                    capture_output=True)
     t0 = time.perf_counter()
-    subprocess.run([exe, "aln", "-i", f"{sub}/q", "-d", f"{root}/db", "-o", f"{sub}/cpu.out"],
-                   check=True, capture_output=True)
+    subprocess.run([exe, "aln", "-i", f"{sub}/q", "-d", f"{root}/db", "-o", f"{sub}/cpu.out"]
+                   + list(aln_args or []), check=True, capture_output=True)
     dt = time.perf_counter() - t0
     from ghostm_amd.aligner import Session
 
-    with Session(["-i", f"{sub}/q", "-d", f"{root}/db", "-o", f"{sub}/gpu.out", "-D", str(_device())]) as s:
+    with Session(["-i", f"{sub}/q", "-d", f"{root}/db", "-o", f"{sub}/gpu.out", "-D", str(_device())]
+                 + list(aln_args or [])) as s:
         s.run()
         gpu = s.output()
         residues = s.stats()["query_residues"]
@@ -81,7 +95,7 @@ def cpu_baseline(root: str, nsample: int, db_res: int, first: int) -> dict:
             else "CPU restatement (oracle/ghostm_oracle.cpp, g++ -O2)")
     return {"value": residues / dt, "unit": "query residues/s", "cores": 1,
             "kind": "reference" if use_ref else "port",
-            "sample": f"first {nsample} queries of rank 0's workload vs the same 10M-residue DB "
+            "sample": f"first {nsample} queries of rank 0's workload vs the same {db_res / 1e6:g}M-residue DB "
                       f"({residues} residues, {dt:.1f} s, {what}, 1 thread)",
             "bit_identical_to_gpu_on_sample": bool(same)}
 
@@ -105,12 +119,20 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--queries", type=int, default=1_000_000, help="queries per rank")
-    ap.add_argument("--db-residues", type=int, default=10_000_000)
+    ap.add_argument("--preset", choices=sorted(PRESETS), default="cfg4",
+                    help="BASELINE.json config (cfg4 = the headline workload)")
+    ap.add_argument("--queries", type=int, default=None, help="queries per rank (default: preset)")
+    ap.add_argument("--db-residues", type=int, default=None)
     ap.add_argument("--cpu-sample", type=int, default=2000)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--workdir", default=None)
     args = ap.parse_args()
+    preset = PRESETS[args.preset]
+    if args.queries is None:
+        args.queries = preset["queries"]
+    if args.db_residues is None:
+        args.db_residues = preset["db"]
+    aln_args = list(preset["aln"])
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -130,9 +152,10 @@ def main() -> None:
     workdir = args.workdir or tempfile.mkdtemp(prefix=f"ghostm_bench_r{rank}_")
     t0 = time.perf_counter()
     first = rank * args.queries
-    make_data(workdir, args.queries, args.db_residues, first)
+    make_data(workdir, args.queries, args.db_residues, first, seed=preset["seed"])
     log(f"[rank {rank}] data ready in {time.perf_counter() - t0:.1f}s at {workdir}")
-    sess = Session(["-i", f"{workdir}/q", "-d", f"{workdir}/db", "-o", f"{workdir}/out", "-D", str(_device())])
+    sess = Session(["-i", f"{workdir}/q", "-d", f"{workdir}/db", "-o", f"{workdir}/out", "-D", str(_device())]
+                   + aln_args)
 
     def step():
         sess.run()
@@ -183,7 +206,7 @@ def main() -> None:
     per = {key: v / k for key, v in st_acc.items()}
     cpu = None
     if rank == 0 and not args.no_cpu:
-        cpu = cpu_baseline(workdir, args.cpu_sample, args.db_residues, first)
+        cpu = cpu_baseline(workdir, args.cpu_sample, args.db_residues, first, preset["seed"], aln_args)
     if rank == 0:
         score_t = per["seconds_score"] / max(1, per["score_launches"])
         score_cells = per["score_cells"] / max(1, per["score_launches"])
@@ -215,9 +238,11 @@ def main() -> None:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": dtype,
-            "data": "synthetic (ghostm synth, splitmix64 seed 4; BLOSUM62 11/1 defaults)",
+            "data": f"synthetic (ghostm synth, splitmix64 seed {preset['seed']}; "
+                    f"aln options {' '.join(aln_args) if aln_args else 'defaults (BLOSUM62 11/1)'})",
             "config": {
-                "workload": "cfg4: synthetic 1M queries (avg 300 aa requested, L=127) x 10M-residue DB, per rank",
+                "workload": preset["workload"],
+                "aln_options": aln_args,
                 "queries_per_rank": args.queries,
                 "db_residues": args.db_residues,
                 "query_residues_per_rank_step": per["query_residues"],
