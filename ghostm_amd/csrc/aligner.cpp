@@ -702,6 +702,7 @@ void Session::Run() {
   stats_.traceback_launches = dt.traceback_launches;
   stats_.traceback_launches_key = dt.traceback_launches_key;
   stats_.seed_runs_hash = dt.seed_launches_hash;
+  stats_.score_rechecks = dt.score_rechecks;
   stats_.seed_bytes = dt.seed_bytes;
   stats_.score_cells = dt.score_cells;
   stats_.traceback_cells = dt.traceback_cells;

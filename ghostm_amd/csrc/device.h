@@ -51,6 +51,7 @@ struct DeviceTimes {
   uint64_t score_cells = 0, traceback_cells = 0;
   uint64_t traceback_launches = 0, traceback_launches_key = 0;
   uint64_t seed_launches_hash = 0;  // Seed() calls whose slot pass used k_seed_hash
+  uint64_t score_rechecks = 0;      // guarded f16 candidates re-scored in int16
 };
 
 class DeviceModule {

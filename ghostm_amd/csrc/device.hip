@@ -105,7 +105,7 @@ struct DeviceModule::Impl {
   std::vector<uint32_t> h_rec_prefix;
   uint64_t ncand = 0;
   // K2 work
-  DevBuf tasks, score_out, end_out;
+  DevBuf tasks, score_out, end_out, guard_list;
   // K3 work
   DevBuf tb_qid, tb_end, tb_start, tb_ml;
   // K4 work
@@ -501,9 +501,12 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
   const bool gaps_ok = gap.open <= 0 && gap.ext <= 0 && -gap.open < 2000 && -gap.ext < 2000;
   const int64_t bound = (int64_t)q->L * max_abs;
   const bool allow_packed = !(force && strcmp(force, "int32") == 0);
-  const bool half = allow_packed && !(force && strcmp(force, "int16") == 0) && gaps_ok && bound < 2048 &&
-                    base + 64 < kDbBack;
   const bool packed = allow_packed && gaps_ok && bound < 30000 && base + 64 < kDbBack;
+  // f16 is exact below 2048; beyond that it runs with a guard and the int16
+  // kernel re-scores the (rare) candidates whose best reaches it
+  const bool half = packed && !(force && strcmp(force, "int16") == 0);
+  int guard = bound < 2048 ? 0 : 2000;
+  if (half && getenv("GHOSTM_K2_GUARD")) guard = atoi(getenv("GHOSTM_K2_GUARD"));  // tests: force re-scores
   const uint32_t per_block = (kern::kScoreBlock / 64) * lay.gpw * (packed ? 2 : 1);
   // tasks: runs of <= per_block consecutive candidates spanning <= Qmax queries
   std::vector<kern::ScoreTask> tasks;
@@ -558,9 +561,16 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
   a.score_out = I.score_out.as<uint32_t>();
   a.end_out = I.end_out.as<uint32_t>();
   a.out_base = cand_begin;
-  I.counters.Reserve(16);
-  HIP_CHECK(hipMemsetAsync(I.counters.p, 0, 16, S(stream_)));
+  I.counters.Reserve(32);
+  HIP_CHECK(hipMemsetAsync(I.counters.p, 0, 32, S(stream_)));
   a.cells = I.counters.as<unsigned long long>();
+  uint32_t *guard_count = reinterpret_cast<uint32_t *>(I.counters.as<unsigned long long>() + 2);
+  if (half && guard) {
+    I.guard_list.Reserve((size_t)n * 8);
+    a.guard = guard;
+    a.guard_count = guard_count;
+    a.guard_list = I.guard_list.as<uint32_t>();
+  }
   const size_t lds = packed ? (size_t)kern::kScoreQmax * kern::kProfRows16 * (lay.Lpad + 8) * 2
                             : (size_t)kern::kScoreQmax * kern::kProfRows * (lay.Lpad + 4) * 4;
   HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
@@ -592,9 +602,36 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
   if (score) HIP_CHECK(hipMemcpyAsync(score, I.score_out.p, n * 4, hipMemcpyDeviceToHost, S(stream_)));
   if (end) HIP_CHECK(hipMemcpyAsync(end, I.end_out.p, n * 4, hipMemcpyDeviceToHost, S(stream_)));
   unsigned long long cells = 0;
+  uint32_t nguard = 0;
   HIP_CHECK(hipMemcpyAsync(&cells, I.counters.p, 8, hipMemcpyDeviceToHost, S(stream_)));
+  HIP_CHECK(hipMemcpyAsync(&nguard, guard_count, 4, hipMemcpyDeviceToHost, S(stream_)));
   HIP_CHECK(hipStreamSynchronize(S(stream_)));
   times_.score += ElapsedMs(I.ev0, I.ev1) * 1e-3;
+  if (half && guard && nguard) {
+    // exact re-score of the guarded candidates with the int16 kernel, one
+    // candidate per work item
+    std::vector<uint32_t> list((size_t)nguard * 2);
+    HIP_CHECK(hipMemcpy(list.data(), I.guard_list.p, list.size() * 4, hipMemcpyDeviceToHost));
+    std::vector<kern::ScoreTask> redo(nguard);
+    for (uint32_t k = 0; k < nguard; ++k)
+      redo[k] = kern::ScoreTask{cand_begin + list[2 * k], 1u, list[2 * k + 1], 1u, 0u};
+    I.tasks.Reserve(redo.size() * sizeof(kern::ScoreTask));
+    HIP_CHECK(hipMemcpy(I.tasks.p, redo.data(), redo.size() * sizeof(kern::ScoreTask), hipMemcpyHostToDevice));
+    kern::ScoreArgs r = a;
+    r.guard = 0;
+    r.cells = I.counters.as<unsigned long long>() + 3;  // not counted twice
+    const dim3 rgrid(nguard);
+    switch (lay.S) {
+      case 32: hipLaunchKernelGGL((kern::k_score16<32, false>), rgrid, block, lds, S(stream_), r); break;
+      case 16: hipLaunchKernelGGL((kern::k_score16<16, false>), rgrid, block, lds, S(stream_), r); break;
+      default: hipLaunchKernelGGL((kern::k_score16<8, false>), rgrid, block, lds, S(stream_), r); break;
+    }
+    HIP_CHECK(hipGetLastError());
+    if (score) HIP_CHECK(hipMemcpyAsync(score, I.score_out.p, n * 4, hipMemcpyDeviceToHost, S(stream_)));
+    if (end) HIP_CHECK(hipMemcpyAsync(end, I.end_out.p, n * 4, hipMemcpyDeviceToHost, S(stream_)));
+    HIP_CHECK(hipStreamSynchronize(S(stream_)));
+    times_.score_rechecks += nguard;
+  }
   times_.score_launches += 1;
   times_.score_launches_packed += packed ? 1 : 0;
   times_.score_launches_half += half ? 1 : 0;

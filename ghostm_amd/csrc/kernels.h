@@ -568,6 +568,11 @@ struct ScoreArgs {
   uint32_t *end_out;
   unsigned long long out_base;
   unsigned long long *cells;  // += L x non-END window columns (work counter)
+  // f16 beyond its exact range: candidates whose best reaches `guard` are
+  // listed (candidate, query) for an exact int16 re-score; guard 0 = off
+  int guard;
+  uint32_t *guard_count;
+  uint32_t *guard_list;
 };
 
 template <int S>
@@ -915,6 +920,20 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16(ScoreArgs a) {
     if (vB) {
       a.score_out[cB - a.out_base] = (uint32_t)BB;
       a.end_out[cB - a.out_base] = offB + (uint32_t)CB;
+    }
+    // every H/E/F is <= the best; f16 holds integers < 2048 exactly, so a best
+    // below the guard is exact, and a true best >= the guard computes >= it
+    if (HALF && a.guard) {
+      if (vA && BA >= a.guard) {
+        const uint32_t k = atomicAdd(a.guard_count, 1u);
+        a.guard_list[2 * k] = (uint32_t)(cA - a.out_base);
+        a.guard_list[2 * k + 1] = t.q_first + slotA;
+      }
+      if (vB && BB >= a.guard) {
+        const uint32_t k = atomicAdd(a.guard_count, 1u);
+        a.guard_list[2 * k] = (uint32_t)(cB - a.out_base);
+        a.guard_list[2 * k + 1] = t.q_first + slotB;
+      }
     }
   }
   WaveAddCells(a.cells, (in_group && i == 0) ? (unsigned long long)((ncols & 0xFFFFu) + (ncols >> 16)) * a.L

@@ -59,6 +59,7 @@ class GhostmStats(ctypes.Structure):
         ("traceback_launches", c_uint64),
         ("traceback_launches_key", c_uint64),
         ("seed_runs_hash", c_uint64),
+        ("score_rechecks", c_uint64),
     ]
 
     def as_dict(self) -> dict:

@@ -141,6 +141,7 @@ typedef struct GhostmStats {
   uint64_t traceback_launches;
   uint64_t traceback_launches_key; /* K3 launches that ran the key formulation */
   uint64_t seed_runs_hash;        /* K1 runs whose slot pass used the hash-count kernel */
+  uint64_t score_rechecks;        /* guarded f16 K2 candidates re-scored exactly in int16 */
 } GhostmStats;
 
 /* Session: parse `aln` options exactly like the reference (getopt string

@@ -207,9 +207,22 @@ def test_default_encoding_is_f16_when_scores_fit(dataset, golden, tmp_path):
     assert st["score_launches_half"] == st["score_launches"] > 0
     assert st["traceback_launches_key"] == st["traceback_launches"] > 0
     assert st["seed_runs_hash"] > 0
+    # PAM250 at L = 127 can reach 2159 > 2047: f16 runs with the re-score guard
     text2, st2 = _gpu_text(d, ["-M", cases.PAM250, "-G", "8", "-E", "1", "-y", "2"], {},
                             str(tmp_path / "p.out"))
-    assert st2["score_launches_half"] == 0 and st2["score_launches_packed"] == st2["score_launches"]
+    assert st2["score_launches_half"] == st2["score_launches_packed"] == st2["score_launches"] > 0
+
+
+@pytest.mark.parametrize("ds,var,opts", [("syn_small", "pam250_g8e1", ["-M", cases.PAM250, "-G", "8", "-E", "1", "-y", "2"]),
+                                         ("syn_small", "default", []), ("syn_dna", "default", [])])
+def test_guarded_f16_rescores_exactly(ds, var, opts, dataset, golden, tmp_path):
+    """With the guard forced low, many candidates go through the int16 re-score
+    path of the guarded f16 kernel; the output is still the golden one."""
+    d = dataset(ds)
+    text, st = _gpu_text(d, opts, {"GHOSTM_K2_GUARD": "25"}, str(tmp_path / "g.out"))
+    (tmp_path / "g.out").write_bytes(text)
+    assert cases.sha256(str(tmp_path / "g.out")) == golden["aln"][f"{ds}/{var}"]["sha256"]
+    assert st["score_rechecks"] > 0 and st["score_launches_half"] == st["score_launches"]
 
 
 REF_GPU_VARIANTS = [v for v in cases.VARIANTS
