@@ -704,7 +704,7 @@ __device__ inline uint32_t W(hf2 v) { return __builtin_bit_cast(uint32_t, v); }
 // lane l receives lane l-1's value (lane 0: 0) — DPP wave_shr:1, a VALU op with
 // no LDS round trip (the group-boundary lanes overwrite it with their own zeros)
 __device__ inline uint32_t ShiftUp(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xF, 0xF, true);  // bound_ctrl: lane 0 reads 0
 }
 
 // Packed cell arithmetic of the two encodings. Scores of both encodings are
@@ -844,15 +844,13 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16(ScoreArgs a) {
   uint32_t hout = 0, fout = 0, hprev = 0;
   uint32_t prev_end = 0xFFFFFFFFu;       // the column before the first one: nothing to carry
   int j = -(int)i;
-  uint32_t jj = (uint32_t)j & 0xFFFFu;
-  jj |= jj << 16;                        // packed column index (both halves)
   // residues two deep: n* = this column's (window-tested), x* = next column's raw
   uint32_t nA = dbp[xA + j], nB = dbp[xB + j];
   nA = (uint32_t)j < wA ? nA : kSeqEnd;
   nB = (uint32_t)j < wB ? nB : kSeqEnd;
   uint32_t pxA = dbp[xA + (uint32_t)(j + 1)], pxB = dbp[xB + (uint32_t)(j + 1)];
   const uint32_t steps = a.base + a.G - 1;
-  for (uint32_t step = 0; step < steps; ++step, ++j, jj += 0x00010001u) {
+  for (uint32_t step = 0; step < steps; ++step, ++j) {
     uint32_t hin = ShiftUp(hout), fin = ShiftUp(fout);
     if (i == 0) { hin = 0; fin = 0; }
     const uint32_t diag0 = hprev;
@@ -891,16 +889,19 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16(ScoreArgs a) {
       // back-to-back dependent packed ops)
       cm = C::Max3(C::Max3(H[k], H[k + 1], H[k + 2]), C::Max3(H[k + 3], H[k + 4], H[k + 5]),
                    C::Max3(H[k + 6], H[k + 7], cm));
+      // keep the next chunk's profile reads from being hoisted above this one
+      // (their registers would push the kernel past 128 VGPRs / 4 waves)
+      __builtin_amdgcn_sched_barrier(0);
     }
     hout = H[S - 1];
     fout = F;
+    // per half: the last column whose max reaches the best (>=), END columns
+    // excluded. Patterns are < 0x8000, so cm - best is negative iff cm < best.
     {
-      const uint32_t cmA = cm & 0xFFFFu, cmB = cm >> 16;
-      uint32_t bA = best & 0xFFFFu, bB = best >> 16, oA = col & 0xFFFFu, oB = col >> 16;
-      if (!(end & 1u)) { if (cmA >= bA) { bA = cmA; oA = (uint32_t)j; } ncols += 1; }
-      if (!(end >> 31)) { if (cmB >= bB) { bB = cmB; oB = (uint32_t)j; } ncols += 0x10000u; }
-      best = bA | (bB << 16);
-      col = oA | (oB << 16);
+      const uint32_t keep = W((S2(cm) - S2(best)) >> (short)15) | end;
+      best = (best & keep) | (cm & ~keep);
+      col = (col & keep) | (MulU24((uint32_t)j & 0xFFFFu, 0x10001u) & ~keep);  // j in both halves
+      ncols += 0x00010001u & ~end;
     }
   }
   int BA = C::Decode(best & 0xFFFFu), CA = (int)(col & 0xFFFFu);
