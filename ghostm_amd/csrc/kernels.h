@@ -1085,6 +1085,13 @@ template <int MLW> struct KeyLayout {
   static constexpr uint32_t kMl = (1u << MLW) - 1;
 };
 
+// (x & m) | (y & ~m) in one v_bfi_b32 (the compiler sometimes splits it)
+__device__ inline uint32_t Bfi(uint32_t m, uint32_t x, uint32_t y) {
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(m), "v"(x), "v"(y));
+  return r;
+}
+
 __device__ inline int ShiftUpI(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xF, 0xF, false); }
 
 template <int S, int MLW>
@@ -1143,32 +1150,41 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
     }
     if (active) {
       const char *rowp = reinterpret_cast<const char *>(s_key) + c * 128;
-      int kd = kdiag0, KF = kfin, kup = kin;
+      auto T = [&](int u) { return *reinterpret_cast<const int *>(rowp + ((qoff[u >> 2] >> (8 * (u & 3))) & 0xFFu)); };
+      int sd = kdiag0 + T(0), KF = kfin, kup = kin;
 #pragma unroll
       for (int k = 0; k < S; k += 4) {
-        // diagonal keys of the chunk from the previous column first, so the rows
-        // below overwrite K in place
+        // diagonal sums of the chunk (and of the next chunk's first row) from the
+        // previous column first, so the rows below overwrite K in place and
+        // nothing but the one sum is carried to the next chunk
         int ks[4];
-        const uint32_t qw = qoff[k >> 2];
+        ks[0] = sd;
 #pragma unroll
-        for (int v = 0; v < 4; ++v)
-          ks[v] = (v == 0 ? kd : K[k + v - 1]) + *reinterpret_cast<const int *>(rowp + ((qw >> (8 * v)) & 0xFFu));
-        kd = K[k + 3];
+        for (int v = 1; v < 4; ++v) ks[v] = K[k + v - 1] + T(k + v);
+        if (k + 4 < S) sd = K[k + 3] + T(k + 4);
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
           const int u = k + v;
-          const int k1 = max(ks[v], KZ);
           const int A = K[u] + OPENK;
-          const int B = (int)((((uint32_t)(KE[u] + EXTK)) & HIGH) | ((uint32_t)A & KL::kLow));
+          const int B = (int)Bfi(HIGH, (uint32_t)(KE[u] + EXTK), (uint32_t)A);
           KE[u] = max(A, B);
           const int AF = kup + OPENKF;
-          const int BF = (int)((((uint32_t)(KF + EXTK)) & HIGH) | ((uint32_t)AF & KL::kLow));
-          KF = max(AF, BF);
-          const int kc = (int)((uint32_t)max(max(k1, KE[u]), KF) & ~KL::kPrio);
+          const int BF = (int)Bfi(HIGH, (uint32_t)(KF + EXTK), (uint32_t)AF);
+          // F floored at the zero key: only values <= 0 change, and those never
+          // beat the zero key (prio 3) nor feed a positive F further down (a
+          // floor extended is ext < 0), so the cell maximum needs no separate
+          // max with the zero key
+          KF = max(max(AF, BF), KZ);
+          const int kc = (int)((uint32_t)max(max(ks[v], KE[u]), KF) & ~KL::kPrio);
           K[u] = kc;
           kup = kc;
           // strict > on h: above the ml field sit h << 2 and the cleared prio
-          if ((kc >> MLW) > (bestK >> MLW)) { bestK = kc; best_col = j; }
+          // (MLW 16: one SDWA compare of the high words; otherwise kc > bestK | kMl,
+          // the same test as floor(kc / 2^MLW) > floor(bestK / 2^MLW))
+          bool better;
+          if constexpr (MLW == 16) better = (kc >> MLW) > (bestK >> MLW);
+          else better = kc > (int)((uint32_t)bestK | KL::kMl);
+          if (better) { bestK = kc; best_col = j; }
         }
       }
       kout = K[S - 1];
