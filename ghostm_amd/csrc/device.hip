@@ -401,11 +401,11 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
   a.gbuf = I.gbuf.as<uint32_t>();
   a.gbuf_off = I.gbuf_off.as<unsigned long long>();
   // K1b pass 1: every class, candidates into per-query slots (largest first).
-  // The LDS classes count bins in a hash table when every bin fits 24 bits
+  // The LDS classes count bins in a hash table when every bin + 2 < 2^21
   // (GHOSTM_K1=merge keeps the merge kernel).
   const char *k1 = getenv("GHOSTM_K1");
   const bool hash = !(k1 && strcmp(k1, "merge") == 0) && d->len > 0 &&
-                    ((uint64_t)(d->len - 1) >> cfg.log_region) + 2 < (1ull << 24);
+                    ((uint64_t)(d->len - 1) >> cfg.log_region) + 2 < kern::kHashBinLimit;
   {
     size_t at = list_total;
     for (int c = 3; c >= 0; --c) {

@@ -315,23 +315,33 @@ __global__ __launch_bounds__(BLOCK) void k_seed(SeedArgs a) {
 //     candidates) without sorting the bins. Each wave walks whole lists, one
 //     position per lane; a position whose bin repeats the previous one of its
 //     list is skipped (each list counts once per bin), the others are counted in
-//     an LDS hash table keyed by bin (linear probing, (bin+1) << 8 | count). A
-//     table scan applies c(b) + c(b+1) >= T, the emitted bins (<= slot_cap) are
-//     ranked by value and written in ascending order. Same output as k_seed in
-//     slot mode; queries with more candidates only get their count here and
-//     are redone by k_seed in offset mode. Needs every bin + 1 < 2^24.
+//     an LDS hash table keyed by bin (linear probing). A table scan applies
+//     c(b) + c(b+1) >= T, the emitted bins (<= slot_cap) are ranked by value and
+//     written in ascending order. Same output as k_seed in slot mode; queries
+//     with more candidates only get their count here and are redone by k_seed in
+//     offset mode. Needs every bin + 2 < 2^21 (kHashBinLimit).
 __device__ inline uint32_t BinHash(uint32_t b) { return b * 2654435761u; }
+constexpr uint32_t kHashBinLimit = 1u << 21;
 
+// Slot word: (bin + 1) << 11 | count << 3, low three bits zero; 0 = empty.
 // Linear probing over slots, read eight at a time: a window is two 4-slot
 // buckets (two 128-bit LDS reads), windows advance by two buckets, wrapping at
 // the table end — the same slot order for inserts and lookups. At load <= 2/3
-// almost every lookup, found or not, ends in its first window.
+// almost every lookup, found or not, ends in its first window. Inside a window
+// (slot ^ key) + m is < 2048 only for the slot holding the bin (m = its index,
+// count above it), and slot + m is < 8 only for an empty one, so both searches
+// are one v_xad / v_add per slot and a min3 tree. A bin is never stored after
+// an empty slot of its probe sequence (no deletions).
 template <uint32_t TSLOTS>
 struct BinTable {
   static constexpr uint32_t kBuckets = TSLOTS / 4;
   uint32_t *tab;
+  __device__ static uint32_t Key(uint32_t b) { return (b + 1) << 11; }
   __device__ static uint32_t Bucket(uint32_t b) { return __umulhi(BinHash(b), kBuckets); }
   __device__ static uint32_t Next(uint32_t k) { return k + 1 == kBuckets ? 0u : k + 1; }
+  __device__ static uint32_t Min8(const uint32_t v[8]) {
+    return min(min(min(v[0], v[1]), v[2]), min(min(min(v[3], v[4]), v[5]), min(v[6], v[7])));
+  }
   // slots of window k in probe order
   __device__ void Window(uint32_t k, uint32_t sl[8], uint32_t *k1) const {
     *k1 = Next(k);
@@ -340,50 +350,56 @@ struct BinTable {
     sl[0] = w0.x; sl[1] = w0.y; sl[2] = w0.z; sl[3] = w0.w;
     sl[4] = w1.x; sl[5] = w1.y; sl[6] = w1.z; sl[7] = w1.w;
   }
-  // first slot of the window holding `key` or empty: 0..7, or 8 if none
-  __device__ static uint32_t FirstMatch(const uint32_t sl[8], uint32_t key, bool *found) {
-    uint32_t pos = 8;
-    *found = false;
+  // min over the window of (slot ^ key) + m: < 2048 iff found (count << 3 | m)
+  __device__ static uint32_t Match(const uint32_t sl[8], uint32_t key) {
+    uint32_t u[8];
 #pragma unroll
-    for (int m = 7; m >= 0; --m) {
-      const bool hitk = (sl[m] & ~0xFFu) == key;
-      if (hitk || sl[m] == 0) { pos = (uint32_t)m; *found = hitk; }
-    }
-    return pos;
+    for (int m = 0; m < 8; ++m) u[m] = (sl[m] ^ key) + (uint32_t)m;
+    return Min8(u);
+  }
+  // first empty slot of the window, or >= 8
+  __device__ static uint32_t Empty(const uint32_t sl[8]) {
+    uint32_t u[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) u[m] = sl[m] + (uint32_t)m;
+    return Min8(u);
   }
   __device__ uint32_t Count(uint32_t b) const {
-    const uint32_t key = (b + 1) << 8;
+    const uint32_t key = Key(b);
     uint32_t k = Bucket(b);
     while (true) {
       uint32_t sl[8], k1;
       Window(k, sl, &k1);
-      bool found;
-      const uint32_t pos = FirstMatch(sl, key, &found);
-      if (pos < 8) return found ? (sl[pos] & 0xFFu) : 0u;
+      const uint32_t mt = Match(sl, key);
+      if (mt < 2048u) return mt >> 3;
+      if (Min8(sl) == 0) return 0;
       k = Next(k1);
     }
   }
+  __device__ uint32_t *Slot(uint32_t k, uint32_t k1, uint32_t m) const {
+    return tab + (m < 4 ? k * 4 + m : k1 * 4 + (m - 4));
+  }
   __device__ void Insert(uint32_t b) {
-    const uint32_t key = (b + 1) << 8;
+    const uint32_t key = Key(b);
     uint32_t k = Bucket(b);
     while (true) {
       uint32_t sl[8], k1;
       Window(k, sl, &k1);
-      bool found;
-      const uint32_t pos = FirstMatch(sl, key, &found);
-      if (pos == 8) {
+      const uint32_t mt = Match(sl, key);
+      if (mt < 2048u) {
+        atomicAdd(Slot(k, k1, mt & 7u), 8u);
+        return;
+      }
+      const uint32_t e = Empty(sl);
+      if (e >= 8) {
         k = Next(k1);
         continue;
       }
-      uint32_t *slot = tab + (pos < 4 ? k * 4 + pos : k1 * 4 + (pos - 4));
-      if (found) {
-        atomicAdd(slot, 1u);
-        return;
-      }
-      const uint32_t old = atomicCAS(slot, 0u, key | 1u);
+      uint32_t *slot = Slot(k, k1, e);
+      const uint32_t old = atomicCAS(slot, 0u, key | 8u);
       if (old == 0) return;
-      if ((old & ~0xFFu) == key) {
-        atomicAdd(slot, 1u);
+      if ((old & ~0x7FFu) == key) {
+        atomicAdd(slot, 8u);
         return;
       }
       // another bin took the slot first: look at the same window again
@@ -394,13 +410,16 @@ struct BinTable {
 template <uint32_t BLOCK, uint32_t TSLOTS>
 __global__ __launch_bounds__(BLOCK) void k_seed_hash(SeedArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];  // TSLOTS words (dynamic)
+  constexpr uint32_t kChunks = TSLOTS / 64;  // the class caps keep n <= TSLOTS
   __shared__ uint32_t s_beg[kMaxLists];
   __shared__ uint32_t s_off[kMaxLists + 1];
+  __shared__ uint8_t s_cfirst[kChunks];      // first list of each 64-entry chunk
   __shared__ __attribute__((aligned(16))) uint32_t s_emit[kMaxSlotCap];
   __shared__ uint32_t s_part[BLOCK / 64];
   __shared__ uint32_t s_total;
   constexpr uint32_t kPer = TSLOTS / BLOCK;
   static_assert(kPer <= 32 && kPer * BLOCK == TSLOTS && TSLOTS % 8 == 0, "table shape");
+  static_assert(kMaxLists <= 256, "list index in a byte");
 
   const uint32_t q = a.query_list[blockIdx.x];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -408,7 +427,6 @@ __global__ __launch_bounds__(BLOCK) void k_seed_hash(SeedArgs a) {
 #pragma unroll
   for (uint32_t k = 0; k < kPer; ++k) s_tab[tid + k * BLOCK] = 0;
   BinTable<TSLOTS> table{s_tab};
-  __syncthreads();
 
   // 1. count. The block's lists are concatenated (s_off = prefix of their
   //    lengths) and cut into 64-entry chunks dealt round-robin to the waves,
@@ -422,7 +440,11 @@ __global__ __launch_bounds__(BLOCK) void k_seed_hash(SeedArgs a) {
     len = a.list_len[(size_t)q * nl + tid];
   }
   const uint32_t excl = BlockExclusiveScan(len, s_part, &s_total);
-  if (tid < nl) s_off[tid] = excl;
+  if (tid < nl) {
+    s_off[tid] = excl;
+    // chunks whose first entry lies in this list
+    for (uint32_t c = (excl + 63) >> 6; (c << 6) < excl + len && c < kChunks; ++c) s_cfirst[c] = (uint8_t)tid;
+  }
   if (tid == 0) s_off[nl] = s_total;
   __syncthreads();
   const uint32_t n = s_off[nl];
@@ -437,9 +459,9 @@ __global__ __launch_bounds__(BLOCK) void k_seed_hash(SeedArgs a) {
       prv[u] = 0xFFFFFFFFu;
       lst[u] = 0xFFFFFFFFu;
       if (i < n) {
-        // list of entry i: first list of the chunk by binary search (uniform),
-        // then at most a few boundaries inside the chunk
-        uint32_t j = UpperIndex(s_off, nl - 1, (c0 + u) << 6);
+        // list of entry i: the chunk's first list, then at most a few
+        // boundaries inside the chunk
+        uint32_t j = c0 + u < kChunks ? s_cfirst[c0 + u] : UpperIndex(s_off, nl - 1, (c0 + u) << 6);
         while (s_off[j + 1] <= i) ++j;
         const uint32_t r = i - s_off[j];
         pos[u] = a.positions[s_beg[j] + r];
@@ -463,17 +485,21 @@ __global__ __launch_bounds__(BLOCK) void k_seed_hash(SeedArgs a) {
   }
   __syncthreads();
 
-  // 2. emission test per occupied slot; the phantom bin 0 (c(0) = 0, c(1) >= T)
+  // 2. emission test per occupied slot (each lane walks only its own occupied
+  //    slots); the phantom bin 0 (c(0) = 0, c(1) >= T)
   const uint32_t thr = a.threshold;
   uint32_t mask = 0, mine = 0;
   bool phantom = false;
   if (thr != 0) {
+    uint32_t occ = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < kPer; ++k) {
+    for (uint32_t k = 0; k < kPer; ++k) occ |= (s_tab[tid + k * BLOCK] != 0 ? 1u : 0u) << k;
+    while (occ) {
+      const uint32_t k = __builtin_ctz(occ);
+      occ &= occ - 1;
       const uint32_t v = s_tab[tid + k * BLOCK];
-      if (v == 0) continue;
-      const uint32_t b = (v >> 8) - 1;
-      if ((v & 0xFFu) + table.Count(b + 1) >= thr) {
+      const uint32_t c = (v >> 3) & 0xFFu;
+      if (c >= thr || c + table.Count(v >> 11) >= thr) {  // bin + 1 = v >> 11
         mask |= 1u << k;
         ++mine;
       }
@@ -491,8 +517,11 @@ __global__ __launch_bounds__(BLOCK) void k_seed_hash(SeedArgs a) {
   // 3. emitted bins -> LDS, rank by value (all distinct), write in order
   uint32_t at = base;
   if (phantom) s_emit[at++] = 0;
-  for (uint32_t k = 0; k < kPer; ++k)
-    if (mask & (1u << k)) s_emit[at++] = (s_tab[tid + k * BLOCK] >> 8) - 1;
+  while (mask) {
+    const uint32_t k = __builtin_ctz(mask);
+    mask &= mask - 1;
+    s_emit[at++] = (s_tab[tid + k * BLOCK] >> 11) - 1;
+  }
   // pad to a multiple of 16 with values above every bin (ranks unaffected)
   for (uint32_t e = total + tid; e < ((total + 15) & ~15u); e += BLOCK) s_emit[e] = 0xFFFFFFFFu;
   __syncthreads();
