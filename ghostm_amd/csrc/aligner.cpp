@@ -706,6 +706,8 @@ void Session::Run() {
   stats_.seed_bytes = dt.seed_bytes;
   stats_.score_cells = dt.score_cells;
   stats_.traceback_cells = dt.traceback_cells;
+  stats_.traceback_launches_scan = dt.traceback_launches_scan;
+  stats_.traceback_scan_cells = dt.traceback_scan_cells;
   for (size_t k = 0; k < used_parts_; ++k)
     for (const auto &h : parts_[k].hits) stats_.hits += h.size();
 }

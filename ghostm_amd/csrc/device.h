@@ -52,6 +52,7 @@ struct DeviceTimes {
   uint64_t traceback_launches = 0, traceback_launches_key = 0;
   uint64_t seed_launches_hash = 0;  // Seed() calls whose slot pass used k_seed_hash
   uint64_t score_rechecks = 0;      // guarded f16 candidates re-scored in int16
+  uint64_t traceback_launches_scan = 0, traceback_scan_cells = 0;  // K3a scores-only pass
 };
 
 class DeviceModule {
@@ -120,7 +121,7 @@ class DeviceModule {
 
  private:
   DeviceModule() = default;
-  void LaunchTraceback(kern::TbArgs a, uint32_t rows, uint32_t n);
+  void LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, const DevDb *d);
   int device_ = -1;
   void *stream_ = nullptr;
   DeviceTimes times_;

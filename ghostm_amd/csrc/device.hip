@@ -77,6 +77,8 @@ thread_local std::string g_last_error;
 
 struct DevQuery {
   DevBuf seq;
+  DevBuf rcodes;                   // K3a row code offsets (kern::k_rev_codes) for rcodes_lpad
+  uint32_t rcodes_lpad = 0;
   uint32_t nseq = 0, L = 0;
   DevBuf group_first, group_last;  // name groups (device merge)
   uint32_t ngroups = 0;
@@ -98,6 +100,7 @@ struct DevDb {
 struct DeviceModule::Impl {
   int h_matrix[32 * 32] = {0};
   DevBuf mat_k2, mat_tb, mat_tbk;  // mat_tbk: two 32x32 key tables (MLW 16, 17)
+  DevBuf mat_raw;                  // the matrix itself (K3a pair table)
   // K1 work
   DevBuf counts, nelem, slots, offsets, qlist, gbuf, gbuf_off, list_beg, list_len;
   DevBuf cand_start, cand_qid;
@@ -106,16 +109,20 @@ struct DeviceModule::Impl {
   uint64_t ncand = 0;
   // K2 work
   DevBuf tasks, score_out, end_out, guard_list;
-  // K3 work
+  // K3 work (tb_sort: two histograms + total, two cursor arrays)
   DevBuf tb_qid, tb_end, tb_start, tb_ml;
+  DevBuf tb_width, tb_ncols, tb_key, tb_order1, tb_order2, tb_sort;
+  int cus = 256;
   // K4 work
   DevBuf keys, sel_count, sel_cand, sel_sid, slot_hits;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  DevBuf counters;  // u64 [0] score cells, [1] traceback cells
+  DevBuf counters;  // u64 [0] score cells, [1] traceback cells, [2] K3a scan cells
   bool matrix_set = false;
 };
 
 static constexpr uint32_t kSlotCap = 256;
+// K3a: the pair table (32 x 32 codes x 32 query codes, one word each) + histogram
+static constexpr size_t kScanLds = (size_t)kern::kPairCodes * 32 * 32 * 4 + kern::kSortBins * 4;
 
 DeviceModule &DeviceModule::Get() {
   static DeviceModule *m = new DeviceModule();
@@ -139,6 +146,18 @@ void DeviceModule::Bind(int device) {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 16384 * 4));
   HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_seed<512, 8192, false>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 8192 * 4));
+  const int scan_lds = (int)kScanLds;
+#define GHOSTM_SCAN_ATTR(SS, HH)                                                                       \
+  HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_tb_scan<SS, HH>,                                 \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, scan_lds));
+  GHOSTM_SCAN_ATTR(32, true) GHOSTM_SCAN_ATTR(32, false) GHOSTM_SCAN_ATTR(16, true)
+  GHOSTM_SCAN_ATTR(16, false) GHOSTM_SCAN_ATTR(8, true) GHOSTM_SCAN_ATTR(8, false)
+#undef GHOSTM_SCAN_ATTR
+  {
+    hipDeviceProp_t p;
+    HIP_CHECK(hipGetDeviceProperties(&p, device));
+    impl_->cus = p.multiProcessorCount > 0 ? p.multiProcessorCount : 256;
+  }
   device_ = device;
 }
 
@@ -184,6 +203,8 @@ void DeviceModule::SetMatrix(const int *m) {
       }
     }
   }
+  impl_->mat_raw.Reserve(sizeof(impl_->h_matrix));
+  HIP_CHECK(hipMemcpy(impl_->mat_raw.p, impl_->h_matrix, sizeof(impl_->h_matrix), hipMemcpyHostToDevice));
   impl_->mat_k2.Reserve(sizeof(k2));
   impl_->mat_tb.Reserve(sizeof(tb));
   impl_->mat_tbk.Reserve(sizeof(tbk));
@@ -229,6 +250,7 @@ DevDb *DeviceModule::UploadDb(const uint8_t *seq, uint32_t len, const uint32_t *
 void DeviceModule::Free(DevQuery *q) {
   if (!q) return;
   q->seq.Release();
+  q->rcodes.Release();
   q->group_first.Release();
   q->group_last.Release();
   delete q;
@@ -640,7 +662,8 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
 
 // K3 launch: the key formulation when its field widths hold (len < 511,
 // matches < 128, |h| < 8192), else the int32 kernel. GHOSTM_K3=int32 forces it.
-void DeviceModule::LaunchTraceback(kern::TbArgs a, uint32_t rows, uint32_t n) {
+void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, const DevDb *d) {
+  const uint32_t rows = q->L;
   Impl &I = *impl_;
   const Layout lay = ChooseLayout(rows, a.base);
   a.Lpad = lay.Lpad;
@@ -659,6 +682,88 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, uint32_t rows, uint32_t n) {
   const bool key17 = !key16 && allow && span < 1000 && hmax < 4000 && -a.open < 2000 && -a.ext < 2000;
   const bool key = key16 || key17;
   if (key) a.mat_tb = I.mat_tbk.as<int>() + (key17 ? 32 * 32 : 0);
+  a.order = nullptr;
+  a.ncols = nullptr;
+  // Two-pass traceback (kernels.h K3a): a scores-only reverse scan finds each
+  // hit's first maximal column j*, then the traceback DP runs columns 0..j*
+  // only, hits sorted by that count. Needs the packed encodings' value range
+  // (as K2): f16 below 2048, int16 below 30000. GHOSTM_K3_SCAN=0 turns it off,
+  // =int16 forces the int16 scan.
+  const char *scan_env = getenv("GHOSTM_K3_SCAN");
+  const bool scan_off = scan_env && strcmp(scan_env, "0") == 0;
+  const bool scan_gaps = a.open <= 0 && a.ext <= 0 && -a.open < 2000 && -a.ext < 2000;
+  const bool scan = !scan_off && n > 0 && scan_gaps && hmax < 30000 && a.base < 65536;
+  if (scan) {
+    const bool half = hmax < 2048 && !(scan_env && strcmp(scan_env, "int16") == 0);
+    const uint32_t NB = kern::kSortBins;
+    I.tb_width.Reserve((size_t)n * 4);
+    I.tb_ncols.Reserve((size_t)n * 4);
+    I.tb_key.Reserve((size_t)n * 4);
+    I.tb_order1.Reserve((size_t)n * 4);
+    I.tb_order2.Reserve((size_t)n * 4);
+    I.tb_sort.Reserve((size_t)(4 * NB + 2) * 4);
+    uint32_t *hist1 = I.tb_sort.as<uint32_t>(), *hist2 = hist1 + NB + 1;
+    uint32_t *cur1 = hist2 + NB + 1, *cur2 = cur1 + NB;
+    HIP_CHECK(hipMemsetAsync(I.tb_sort.p, 0, (size_t)(4 * NB + 2) * 4, S(stream_)));
+    const dim3 g256((n + 255) / 256), b256(256);
+    const uint32_t *subj = d && d->nsubj ? d->subj.as<uint32_t>() : nullptr;
+    hipLaunchKernelGGL(kern::k_tb_prep, g256, b256, 0, S(stream_), a.qid, a.end, n, a.base, subj,
+                       subj ? d->nsubj : 0u, d ? d->len : 0u, I.tb_width.as<uint32_t>(),
+                       I.tb_ncols.as<uint32_t>(), I.tb_key.as<uint32_t>(), hist1, hist2);  // empty -> hist2[0]
+    hipLaunchKernelGGL(kern::k_csort_scatter, g256, b256, 0, S(stream_), I.tb_key.as<uint32_t>(), n, true,
+                       hist1, cur1, I.tb_order1.as<uint32_t>());
+    kern::TbScanArgs sa{};
+    sa.qseq = a.qseq;
+    sa.L = a.L;
+    sa.Lpad = lay.Lpad;
+    sa.G = lay.G;
+    sa.gpw = lay.gpw;
+    sa.db = a.db;
+    sa.mat = I.mat_raw.as<int>();
+    sa.qid = a.qid;
+    sa.end = a.end;
+    sa.width = I.tb_width.as<uint32_t>();
+    sa.key = I.tb_key.as<uint32_t>();
+    if (q->rcodes_lpad != lay.Lpad) {
+      q->rcodes.Reserve((size_t)q->nseq * lay.Lpad + 16);
+      const size_t words = (size_t)q->nseq * (lay.Lpad / 4);
+      if (words)
+        hipLaunchKernelGGL(kern::k_rev_codes, dim3((uint32_t)((words + 255) / 256)), b256, 0, S(stream_),
+                           q->seq.as<uint8_t>(), q->nseq, q->L, lay.Lpad, q->rcodes.as<uint32_t>());
+      q->rcodes_lpad = lay.Lpad;
+    }
+    sa.rcodes = q->rcodes.as<uint32_t>();
+    sa.n = n;
+    sa.base = a.base;
+    sa.items = I.tb_order1.as<uint32_t>();
+    sa.item_total = hist1 + NB;
+    sa.open = a.open;
+    sa.ext = a.ext;
+    sa.ncols = I.tb_ncols.as<uint32_t>();
+    sa.hist = hist2;
+    sa.cells = a.cells ? a.cells + 1 : nullptr;
+    // every CU one 1024-thread workgroup, looping over the sorted pairs
+    const uint32_t pairs_per_block = (kern::kScanBlock / 64) * lay.gpw;
+    const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)I.cus,
+                                                                     (n + pairs_per_block - 1) / pairs_per_block));
+#define GHOSTM_SCAN(SS)                                                                                      \
+  if (half) hipLaunchKernelGGL((kern::k_tb_scan<SS, true>), dim3(blocks), dim3(kern::kScanBlock), kScanLds,   \
+                               S(stream_), sa);                                                              \
+  else hipLaunchKernelGGL((kern::k_tb_scan<SS, false>), dim3(blocks), dim3(kern::kScanBlock), kScanLds,       \
+                          S(stream_), sa);
+    switch (lay.S) {
+      case 32: GHOSTM_SCAN(32); break;
+      case 16: GHOSTM_SCAN(16); break;
+      default: GHOSTM_SCAN(8); break;
+    }
+#undef GHOSTM_SCAN
+    hipLaunchKernelGGL(kern::k_csort_scatter, g256, b256, 0, S(stream_), I.tb_ncols.as<uint32_t>(), n, false,
+                       hist2, cur2, I.tb_order2.as<uint32_t>());
+    HIP_CHECK(hipGetLastError());
+    a.order = I.tb_order2.as<uint32_t>();
+    a.ncols = I.tb_ncols.as<uint32_t>();
+    times_.traceback_launches_scan += 1;
+  }
   const uint32_t per_block = (kern::kTbBlock / 64) * lay.gpw;
   const dim3 grid((n + per_block - 1) / per_block), block(kern::kTbBlock);
 #define GHOSTM_TB(SS)                                                                        \
@@ -738,11 +843,11 @@ void DeviceModule::MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, 
   a.ext = ext;
   a.out_start = I.tb_start.as<uint32_t>();
   a.out_ml = I.tb_ml.as<uint32_t>();
-  I.counters.Reserve(16);
-  HIP_CHECK(hipMemsetAsync(I.counters.p, 0, 16, S(stream_)));
+  I.counters.Reserve(32);
+  HIP_CHECK(hipMemsetAsync(I.counters.p, 0, 24, S(stream_)));
   a.cells = I.counters.as<unsigned long long>() + 1;
   HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
-  LaunchTraceback(a, q->L, (uint32_t)slots);
+  LaunchTraceback(a, q, (uint32_t)slots, d);
   HIP_CHECK(hipEventRecord(I.ev1, S(stream_)));
   hipLaunchKernelGGL(kern::k_finalize, dim3((uint32_t)((slots + 255) / 256)), dim3(256), 0, S(stream_),
                      I.sel_count.as<uint32_t>(), I.sel_cand.as<uint32_t>(), I.sel_sid.as<uint32_t>(),
@@ -756,10 +861,14 @@ void DeviceModule::MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, 
   HIP_CHECK(hipMemcpyAsync(counts->data(), I.sel_count.p, (size_t)ng * 4, hipMemcpyDeviceToHost, S(stream_)));
   HIP_CHECK(hipMemcpyAsync(hits->data(), I.slot_hits.p, slots * sizeof(SelectedHit), hipMemcpyDeviceToHost,
                            S(stream_)));
+  unsigned long long scan_cells = 0;
   HIP_CHECK(hipMemcpyAsync(&cells, I.counters.as<unsigned long long>() + 1, 8, hipMemcpyDeviceToHost, S(stream_)));
+  HIP_CHECK(hipMemcpyAsync(&scan_cells, I.counters.as<unsigned long long>() + 2, 8, hipMemcpyDeviceToHost,
+                           S(stream_)));
   HIP_CHECK(hipStreamSynchronize(S(stream_)));
   times_.traceback += ElapsedMs(I.ev0, I.ev1) * 1e-3;
   times_.traceback_cells += cells;
+  times_.traceback_scan_cells += scan_cells;
 }
 
 void DeviceModule::ResetRecords() { records_ = 0; }
@@ -845,20 +954,24 @@ void DeviceModule::TraceBack(DevQuery *q, DevDb *d, uint32_t n, const uint32_t *
   a.ext = ext;
   a.out_start = I.tb_start.as<uint32_t>();
   a.out_ml = I.tb_ml.as<uint32_t>();
-  I.counters.Reserve(16);
-  HIP_CHECK(hipMemsetAsync(I.counters.p, 0, 16, S(stream_)));
+  I.counters.Reserve(32);
+  HIP_CHECK(hipMemsetAsync(I.counters.p, 0, 24, S(stream_)));
   a.cells = I.counters.as<unsigned long long>() + 1;
   HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
-  LaunchTraceback(a, q->L, n);
+  LaunchTraceback(a, q, n, d);
   HIP_CHECK(hipEventRecord(I.ev1, S(stream_)));
   std::vector<uint32_t> ml(n);
   HIP_CHECK(hipMemcpyAsync(db_start, I.tb_start.p, (size_t)n * 4, hipMemcpyDeviceToHost, S(stream_)));
   HIP_CHECK(hipMemcpyAsync(ml.data(), I.tb_ml.p, (size_t)n * 4, hipMemcpyDeviceToHost, S(stream_)));
   unsigned long long cells = 0;
+  unsigned long long scan_cells = 0;
   HIP_CHECK(hipMemcpyAsync(&cells, I.counters.as<unsigned long long>() + 1, 8, hipMemcpyDeviceToHost, S(stream_)));
+  HIP_CHECK(hipMemcpyAsync(&scan_cells, I.counters.as<unsigned long long>() + 2, 8, hipMemcpyDeviceToHost,
+                           S(stream_)));
   HIP_CHECK(hipStreamSynchronize(S(stream_)));
   times_.traceback += ElapsedMs(I.ev0, I.ev1) * 1e-3;
   times_.traceback_cells += cells;
+  times_.traceback_scan_cells += scan_cells;
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t len = ml[i] >> 8, match = ml[i] & 0xFFu;
     if (aln_len) aln_len[i] = len;

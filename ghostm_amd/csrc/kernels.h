@@ -986,7 +986,18 @@ struct TbArgs {
   uint32_t *out_start;
   uint32_t *out_ml;           // (aln_len << 8) | matches
   unsigned long long *cells;  // += L x processed columns (work counter)
+  // two-pass traceback (K3a k_tb_scan first): hits in the order given (sorted
+  // by their column count) and each hit's DP stopped after ncols[hit] columns;
+  // null = slot order, the whole window
+  const uint32_t *order;
+  const uint32_t *ncols;
 };
+
+// the wave's largest value (loop bound of a lane-group loop)
+__device__ inline uint32_t WaveMax(uint32_t v) {
+  for (int d = 32; d > 0; d >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, d));
+  return v;
+}
 
 template <int S>
 __global__ __launch_bounds__(kTbBlock) void k_traceback(TbArgs a) {
@@ -996,8 +1007,10 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback(TbArgs a) {
 
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t g = lane / a.G, i = lane - g * a.G;
-  const uint32_t hit = (blockIdx.x * (kTbBlock / 64) + wave) * a.gpw + g;
-  const bool valid = g < a.gpw && hit < a.n && a.qid[hit] != 0xFFFFFFFFu;
+  const uint32_t idx = (blockIdx.x * (kTbBlock / 64) + wave) * a.gpw + g;
+  const bool in_range = g < a.gpw && idx < a.n;
+  const uint32_t hit = in_range && a.order ? a.order[idx] : idx;
+  const bool valid = in_range && a.qid[hit] != 0xFFFFFFFFu;
   uint32_t p0 = 0, width = 0;
   // processing row U = i*S + u walks the query backwards: position L-1-(U-pad)
   uint32_t qcode[S / 4];
@@ -1006,6 +1019,7 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback(TbArgs a) {
   if (valid) {
     p0 = a.end[hit];
     width = p0 < a.base ? p0 + 1 : a.base;
+    if (a.ncols) width = min(width, a.ncols[hit]);
     const uint8_t *qs = a.qseq + (size_t)a.qid[hit] * a.L;
 #pragma unroll
     for (int u = 0; u < S; ++u) {
@@ -1023,7 +1037,8 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback(TbArgs a) {
   uint32_t ncols = 0;
   const int open = a.open, ext = a.ext;
   int j = -(int)i;
-  const uint32_t steps = a.base + a.G - 1;
+  const uint32_t wmax = WaveMax(valid ? width : 0u);
+  const uint32_t steps = wmax ? wmax + a.G - 1 : 0u;
   for (uint32_t step = 0; step < steps; ++step, ++j) {
     int hin = __shfl_up(hout, 1), fin = __shfl_up(fout, 1), min_ = __shfl_up(mout, 1);
     if (i == 0) { hin = 0; fin = 0; min_ = 0; }
@@ -1132,8 +1147,10 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
 
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t g = lane / a.G, i = lane - g * a.G;
-  const uint32_t hit = (blockIdx.x * (kTbBlock / 64) + wave) * a.gpw + g;
-  const bool valid = g < a.gpw && hit < a.n && a.qid[hit] != 0xFFFFFFFFu;
+  const uint32_t idx = (blockIdx.x * (kTbBlock / 64) + wave) * a.gpw + g;
+  const bool in_range = g < a.gpw && idx < a.n;
+  const uint32_t hit = in_range && a.order ? a.order[idx] : idx;
+  const bool valid = in_range && a.qid[hit] != 0xFFFFFFFFu;
   uint32_t p0 = 0, width = 0;
   // byte offset (code * 4) of processing row U = i*S + u's query code inside a
   // table row, four rows per register; row U walks the query backwards:
@@ -1144,6 +1161,7 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
   if (valid) {
     p0 = a.end[hit];
     width = p0 < a.base ? p0 + 1 : a.base;
+    if (a.ncols) width = min(width, a.ncols[hit]);
     const uint8_t *qs = a.qseq + (size_t)a.qid[hit] * a.L;
 #pragma unroll
     for (int u = 0; u < S; ++u) {
@@ -1165,7 +1183,8 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
   const int KZ = (int)(3u << MLW);
   const uint32_t HIGH = ~KL::kLow;
   int j = -(int)i;
-  const uint32_t steps = a.base + a.G - 1;
+  const uint32_t wmax = WaveMax(valid ? width : 0u);
+  const uint32_t steps = wmax ? wmax + a.G - 1 : 0u;
   for (uint32_t step = 0; step < steps; ++step, ++j) {
     int kin = ShiftUpI(kout), kfin = ShiftUpI(kfout);
     if (i == 0) { kin = 0; kfin = 0; }
@@ -1351,6 +1370,298 @@ __global__ void k_records(const uint32_t *sel_count, const SlotHit *slots, const
     out[at + k] = HitRecord32{qid, d_base + h.sid, h.score, h.start, h.end, len, match,
                               (float)match / (float)len};
   }
+}
+
+
+// ------------------------------------------------------------------ K3a scan
+// Two-pass traceback. The reverse DP's first maximal cell lies in column j*, the
+// first column whose maximum reaches the hit's best (strict >, aligner.cpp:898).
+// The DP is causal in column order, so the key kernel run over columns 0..j*
+// alone computes the same cells there and finds the same first maximal cell:
+// start, length and matches are unchanged. j* is found by a cheaper scores-only
+// pass, k_tb_scan: the K2 cell arithmetic (two hits per lane in the 16-bit
+// halves, f16 holding exact integers or int16), scanning the reverse window.
+// On the synthetic workload j* + 1 averages ~44 of ~180 window columns, and the
+// scores-only pass costs about a third of the key DP per column.
+//
+// Work is balanced by sorting: k_tb_prep computes each hit's reverse window
+// (the reverse scan stops at the subject's first residue: aligner.cpp:801-812)
+// and pairs hits of one query; k_csort_scatter orders the pairs by width for
+// k_tb_scan and the hits by j* + 1 for the key kernel, so each wave's lane
+// groups run windows of about the same length.
+constexpr uint32_t kSortBins = 1024;   // counting-sort keys (column counts), clamped
+constexpr int kScanBlock = 1024;       // one workgroup per CU: the pair table fills the LDS
+constexpr uint32_t kPairCodes = 26;    // DB codes 0..25 (25 = END) index the pair table
+
+// Per slot: the reverse window (0 = empty slot; counted into *empty), ncols reset to 0; per item
+// (= its first slot): the pair key, counted into hist[key] and hist[kSortBins]
+// (total). A pair is slots (2m, 2m+1) of the same query; an odd slot whose
+// query equals its even neighbour's belongs to that pair and is no item.
+__global__ __launch_bounds__(256) void k_tb_prep(const uint32_t *qid, const uint32_t *end, uint32_t n,
+                                                 uint32_t base, const uint32_t *subj, uint32_t nsubj,
+                                                 uint32_t dblen, uint32_t *width, uint32_t *ncols,
+                                                 uint32_t *key, uint32_t *hist, uint32_t *empty) {
+  __shared__ uint32_t s_hist[kSortBins];
+  __shared__ uint32_t s_total, s_empty;
+  for (uint32_t b = threadIdx.x; b < kSortBins; b += blockDim.x) s_hist[b] = 0;
+  if (threadIdx.x == 0) { s_total = 0; s_empty = 0; }
+  __syncthreads();
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  auto window = [&](uint32_t s) -> uint32_t {
+    if (qid[s] == 0xFFFFFFFFu) return 0;
+    const uint32_t p0 = end[s];
+    uint32_t w = p0 < base ? p0 + 1 : base;
+    if (nsubj) {
+      const uint32_t sid = SubjectOf(subj, nsubj, dblen, p0);
+      if (sid != 0xFFFFFFFFu) w = min(w, p0 - subj[sid] + 1);
+    }
+    return w;
+  };
+  if (k < n) {
+    const uint32_t w = window(k);
+    width[k] = w;
+    ncols[k] = 0;
+    if (!w) atomicAdd(&s_empty, 1u);
+    const uint32_t q = qid[k];
+    uint32_t item = w;
+    if (w && (k & 1) && qid[k - 1] == q) item = 0;           // the even slot's partner
+    if (w && !(k & 1) && k + 1 < n && qid[k + 1] == q) item = max(w, window(k + 1));
+    key[k] = min(item, kSortBins - 1);
+    if (item) {
+      atomicAdd(&s_hist[min(item, kSortBins - 1)], 1u);
+      atomicAdd(&s_total, 1u);
+    }
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < kSortBins; b += blockDim.x)
+    if (s_hist[b]) atomicAdd(&hist[b], s_hist[b]);
+  if (threadIdx.x == 0 && s_total) atomicAdd(&hist[kSortBins], s_total);
+  if (threadIdx.x == 0 && s_empty) atomicAdd(empty, s_empty);
+}
+
+// Counting-sort scatter: order[prefix(key) + rank] = index, for every index with
+// key > 0 (skip_zero) or every index. hist holds the key counts; cursor (zeroed)
+// hands out the ranks, one global atomic per (block, key).
+__global__ __launch_bounds__(256) void k_csort_scatter(const uint32_t *key, uint32_t n, bool skip_zero,
+                                                       const uint32_t *hist, uint32_t *cursor,
+                                                       uint32_t *order) {
+  __shared__ uint32_t s_pre[kSortBins];
+  __shared__ uint32_t s_cnt[kSortBins];
+  __shared__ uint32_t s_part[256];
+  // exclusive prefix of the histogram: 4 bins per thread, then the 256 partials
+  const uint32_t t = threadIdx.x;
+  uint32_t v[4], sum = 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const uint32_t b = t * 4 + u;
+    v[u] = (skip_zero && b == 0) ? 0u : hist[b];
+    sum += v[u];
+    s_cnt[b] = 0;
+  }
+  s_part[t] = sum;
+  __syncthreads();
+  for (uint32_t d = 1; d < 256; d <<= 1) {
+    const uint32_t x = t >= d ? s_part[t - d] : 0u;
+    __syncthreads();
+    s_part[t] += x;
+    __syncthreads();
+  }
+  uint32_t run = s_part[t] - sum;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    s_pre[t * 4 + u] = run;
+    run += v[u];
+  }
+  __syncthreads();
+  const uint32_t k = blockIdx.x * blockDim.x + t;
+  uint32_t b = 0, rank = 0;
+  const bool take = k < n && (!skip_zero || key[k] != 0);
+  if (take) {
+    b = min(key[k], kSortBins - 1);
+    rank = atomicAdd(&s_cnt[b], 1u);
+  }
+  __syncthreads();
+  for (uint32_t x = t; x < kSortBins; x += blockDim.x)
+    if (s_cnt[x]) s_cnt[x] = atomicAdd(&cursor[x], s_cnt[x]);
+  __syncthreads();
+  if (take) order[s_pre[b] + s_cnt[b] + rank] = k;
+}
+
+struct TbScanArgs {
+  const uint8_t *qseq;
+  uint32_t L, Lpad, G, gpw;
+  const uint8_t *db;
+  const int *mat;              // 32x32 substitution matrix (row = DB code)
+  const uint32_t *qid, *end;   // per slot
+  const uint32_t *width;       // per slot, from k_tb_prep
+  const uint32_t *key;         // per item (its first slot), from k_tb_prep
+  const uint32_t *rcodes;      // k_rev_codes: per query Lpad/4 words of row code offsets
+  uint32_t n, base;            // slots; reverse window limit
+  const uint32_t *items;       // pair items sorted by width; count in item_total[0]
+  const uint32_t *item_total;
+  int open, ext;
+  uint32_t *ncols;             // per slot: j* + 1
+  uint32_t *hist;              // histogram of ncols (kSortBins)
+  unsigned long long *cells;   // += L x scanned columns
+};
+
+// Per query, the table byte offsets (code * 4) of its rows in the reverse DP's
+// processing order (row U at position Lpad-1-U; padding rows kPadCode), four per
+// word: lane i of a lane group reads its S/4 words as aligned 16-byte loads.
+__global__ void k_rev_codes(const uint8_t *qseq, uint32_t nq, uint32_t L, uint32_t Lpad, uint32_t *out) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t words = Lpad / 4;
+  if (t >= (size_t)nq * words) return;
+  const size_t q = t / words;
+  const uint32_t w = (uint32_t)(t - q * words);
+  uint32_t word = 0;
+  for (uint32_t v = 0; v < 4; ++v) {
+    const uint32_t k = Lpad - 1 - (4 * w + v);
+    word |= (k < L ? (uint32_t)qseq[q * L + k] * 4 : kPadCode * 4) << (8 * v);
+  }
+  out[t] = word;
+}
+
+// Pair table in LDS: word (a, b, q) = (M[a][q], M[b][q]) encoded in the two
+// halves; the byte offset ((a * 32 + b) << 7) + 4q is one SDWA add per row, and
+// one ds_read_b32 gives both hits' profile values, with no v_perm.
+template <int S, bool HALF>
+__global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
+  using C = Cells<HALF>;
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_pair[];
+  uint32_t *s_hist = s_pair + kPairCodes * 32 * 32;
+  for (uint32_t e = threadIdx.x; e < kPairCodes * 32 * 32; e += kScanBlock) {
+    const uint32_t q = e & 31, cb = (e >> 5) & 31, ca = e >> 10;
+    const int va = q == kPadCode ? kNeg16 : (ca < 25 && q < 25 ? a.mat[ca * 32 + q] : 0);
+    const int vb = q == kPadCode ? kNeg16 : (cb < 25 && q < 25 ? a.mat[cb * 32 + q] : 0);
+    s_pair[e] = (uint32_t)(unsigned short)C::Encode(va) | (uint32_t)(unsigned short)C::Encode(vb) << 16;
+  }
+  for (uint32_t b = threadIdx.x; b < kSortBins; b += kScanBlock) s_hist[b] = 0;
+  __syncthreads();
+
+  const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t g = lane / a.G, i = lane - g * a.G;
+  const uint32_t nitems = a.item_total[0];
+  const uint32_t stride = gridDim.x * (kScanBlock / 64) * a.gpw;
+  const C cell(a.open, a.ext);
+  for (uint32_t first = (blockIdx.x * (kScanBlock / 64) + wave) * a.gpw; first < nitems; first += stride) {
+    const uint32_t it = first + g;
+    uint32_t sA = 0xFFFFFFFFu, sB = 0xFFFFFFFFu, wA = 0, wB = 0, p0A = 0, p0B = 0, q = 0;
+    if (g < a.gpw && it < nitems) {
+      sA = a.items[it];
+      q = a.qid[sA];
+      wA = a.width[sA];
+      p0A = a.end[sA];
+      if (!(sA & 1) && sA + 1 < a.n && a.qid[sA + 1] == q && a.width[sA + 1]) {
+        sB = sA + 1;
+        wB = a.width[sB];
+        p0B = a.end[sB];
+      }
+    }
+    // query byte offsets (code * 4), processing row U = i*S + u at position Lpad-1-U
+    // (k_rev_codes has them packed per query: S/4 aligned words per lane)
+    uint32_t qoff[S / 4];
+    {
+      const uint32_t *rw = a.rcodes + (size_t)(wA ? q : 0u) * (a.Lpad / 4) + i * (S / 4);
+      if constexpr (S >= 16) {
+#pragma unroll
+        for (int w = 0; w < S / 16; ++w) {
+          const uint4 v = reinterpret_cast<const uint4 *>(rw)[w];
+          qoff[4 * w] = v.x;
+          qoff[4 * w + 1] = v.y;
+          qoff[4 * w + 2] = v.z;
+          qoff[4 * w + 3] = v.w;
+        }
+      } else {
+        const uint2 v = *reinterpret_cast<const uint2 *>(rw);  // S = 8: two words
+        qoff[0] = v.x;
+        qoff[1] = v.y;
+      }
+    }
+    uint32_t H[S], E[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) { H[k] = 0; E[k] = 0; }
+    uint32_t best = 0, col = 0;                 // packed halves
+    uint32_t dead = (wA ? 0u : 0x0000FFFFu) | (wB ? 0u : 0xFFFF0000u);
+    uint32_t hout = 0, fout = 0, hprev = 0, prev_end = 0xFFFFFFFFu;
+    int j = -(int)i;
+    // items ascend by key = max(wA, wB): the batch's last item has the longest
+    // window (a clamped key stands for the whole window)
+    const uint32_t last = a.items[min(first + a.gpw, nitems) - 1];
+    uint32_t wmax = __builtin_amdgcn_readfirstlane(a.key[last]);
+    if (wmax >= kSortBins - 1) wmax = a.base;
+    const uint32_t steps = wmax + a.G - 1;
+    // residues of the reverse window, one column ahead; outside the window (fill:
+    // j < 0, beyond: its end or the subject's start) a column behaves as END.
+    // The load address stays inside the window (p0 itself when outside).
+    auto fetch = [&](int jj, uint32_t p0, uint32_t w) -> uint32_t {
+      const bool in = jj >= 0 && (uint32_t)jj < w;
+      const uint32_t x = a.db[p0 - (in ? (uint32_t)jj : 0u)];
+      return in ? x : kSeqEnd;
+    };
+    uint32_t nA = fetch(j, p0A, wA), nB = fetch(j, p0B, wB);
+    for (uint32_t step = 0; step < steps; ++step, ++j) {
+      uint32_t hin = ShiftUp(hout), fin = ShiftUp(fout);
+      if (i == 0) { hin = 0; fin = 0; }
+      const uint32_t diag0 = hprev;
+      hprev = hin;
+      const uint32_t rA = nA, rB = nB;
+      nA = fetch(j + 1, p0A, wA);
+      nB = fetch(j + 1, p0B, wB);
+      const uint32_t end = (rA == kSeqEnd ? 0x0000FFFFu : 0u) | (rB == kSeqEnd ? 0xFFFF0000u : 0u);
+      if (j >= 0) dead |= end;                  // the reference breaks at END
+      const typename C::Step st = cell.At(end, prev_end);
+      prev_end = end;
+      const uint32_t cbase = (min(rA, kPairCodes - 1) << 12) | (rB << 7);
+      const char *tp = reinterpret_cast<const char *>(s_pair) + cbase;
+      auto T = [&](int u) { return *reinterpret_cast<const uint32_t *>(tp + ((qoff[u >> 2] >> (8 * (u & 3))) & 0xFFu)); };
+      uint32_t diag = diag0, F = fin, cm = 0;
+#pragma unroll
+      for (int k = 0; k < S; k += 8) {
+        // the chunk's eight table reads issued together, then their sums
+        uint32_t t[8], s[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = T(k + u);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s[u] = C::Diag(u == 0 ? diag : H[k + u - 1], st.m, t[u]);
+        diag = H[k + 7];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) C::Row(st, s[u], H[k + u], E[k + u], F);
+        cm = C::Max3(C::Max3(H[k], H[k + 1], H[k + 2]), C::Max3(H[k + 3], H[k + 4], H[k + 5]),
+                     C::Max3(H[k + 6], H[k + 7], cm));
+        // the next chunk's table reads stay behind this one (register budget)
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      hout = H[S - 1];
+      fout = F;
+      // strict first maximum per live half: best - cm < 0 iff cm > best
+      const uint32_t upd = W((S2(best) - S2(cm)) >> (short)15) & ~(end | dead);
+      best = (best & ~upd) | (cm & upd);
+      col = (col & ~upd) | (((uint32_t)j & 0xFFFFu) * 0x10001u & upd);
+    }
+    int BA = C::Decode(best & 0xFFFFu), CA = (int)(col & 0xFFFFu);
+    int BB = C::Decode(best >> 16), CB = (int)(col >> 16);
+    // first column over the group's row strips
+    for (uint32_t k = 1; k < a.G; ++k) {
+      const int src = (int)(g * a.G + k);
+      const int oba = __shfl(BA, src), oca = __shfl(CA, src);
+      const int obb = __shfl(BB, src), ocb = __shfl(CB, src);
+      if (oba > BA || (oba == BA && oca < CA)) { BA = oba; CA = oca; }
+      if (obb > BB || (obb == BB && ocb < CB)) { BB = obb; CB = ocb; }
+    }
+    if (i == 0 && wA) {
+      a.ncols[sA] = (uint32_t)CA + 1;
+      atomicAdd(&s_hist[min((uint32_t)CA + 1, kSortBins - 1)], 1u);
+      if (wB) {
+        a.ncols[sB] = (uint32_t)CB + 1;
+        atomicAdd(&s_hist[min((uint32_t)CB + 1, kSortBins - 1)], 1u);
+      }
+    }
+    WaveAddCells(a.cells, i == 0 ? (unsigned long long)(wA + wB) * a.L : 0ull);
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < kSortBins; b += kScanBlock)
+    if (s_hist[b]) atomicAdd(&a.hist[b], s_hist[b]);
 }
 
 }  // namespace kern

@@ -60,6 +60,8 @@ class GhostmStats(ctypes.Structure):
         ("traceback_launches_key", c_uint64),
         ("seed_runs_hash", c_uint64),
         ("score_rechecks", c_uint64),
+        ("traceback_launches_scan", c_uint64),
+        ("traceback_scan_cells", c_uint64),
     ]
 
     def as_dict(self) -> dict:

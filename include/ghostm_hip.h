@@ -142,6 +142,8 @@ typedef struct GhostmStats {
   uint64_t traceback_launches_key; /* K3 launches that ran the key formulation */
   uint64_t seed_runs_hash;        /* K1 runs whose slot pass used the hash-count kernel */
   uint64_t score_rechecks;        /* guarded f16 K2 candidates re-scored exactly in int16 */
+  uint64_t traceback_launches_scan; /* K3 launches preceded by the scores-only scan (K3a) */
+  uint64_t traceback_scan_cells;    /* K3a: sum over hits of L x reverse-window columns */
 } GhostmStats;
 
 /* Session: parse `aln` options exactly like the reference (getopt string

@@ -62,6 +62,21 @@ __global__ void k(uint64_t *cyc, uint32_t *sink) {
     if constexpr (OP == 10) DEP8("v_pk_max_i16");
     if constexpr (OP == 11) DEP8("v_max_i32");
     if constexpr (OP == 12) DEP8T("v_pk_sub_u16", " clamp");
+    // float forms: does the f32 datapath issue wave64 in 2 cycles (SIMD-32)?
+    if constexpr (OP == 13) OP8("v_add_f32");
+    if constexpr (OP == 14) OP8("v_max_f32");
+    if constexpr (OP == 15) OP8_3("v_max3_f32", "");
+    if constexpr (OP == 16) OP8_3("v_fma_f32", "");
+    if constexpr (OP == 17) OP8("v_pk_add_f16");
+    if constexpr (OP == 18) OP8_3("v_pk_maximum3_f16", "");
+    if constexpr (OP == 19) OP8_3("v_pk_fma_f16", "");
+    if constexpr (OP == 20) OP8("v_add_u32");
+    if constexpr (OP == 21) OP8_3("v_max3_u32", "");
+    if constexpr (OP == 23) OP8("v_mul_f32");
+    if constexpr (OP == 25) DEP8("v_add_f32");
+    if constexpr (OP == 26) OP8_3("v_med3_f32", "");
+    if constexpr (OP == 27) OP8_3("v_max3_i16", "");
+    if constexpr (OP == 28) OP8("v_max_f16");
   }
   uint64_t t1 = __builtin_readcyclecounter();
   if (threadIdx.x % 64 == 0) cyc[blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64] = t1 - t0;
@@ -105,7 +120,26 @@ int run(const char *name, int instr_per_iter, int waves_per_simd) {
   return 0;
 }
 
-int main() {
+int main(int argc, char **argv) {
+  if (argc > 1) {  // float set only
+    for (int w : {1, 2, 4, 8}) {
+      run<13>("v_add_f32 x8", 8, w);
+      run<23>("v_mul_f32 x8", 8, w);
+      run<14>("v_max_f32 x8", 8, w);
+      run<15>("v_max3_f32 x8", 8, w);
+      run<26>("v_med3_f32 x8", 8, w);
+      run<16>("v_fma_f32 x8", 8, w);
+      run<17>("v_pk_add_f16 x8", 8, w);
+      run<18>("v_pk_maximum3_f16 x8", 8, w);
+      run<19>("v_pk_fma_f16 x8", 8, w);
+      run<28>("v_max_f16 x8", 8, w);
+      run<27>("v_max3_i16 x8", 8, w);
+      run<20>("v_add_u32 x8", 8, w);
+      run<21>("v_max3_u32 x8", 8, w);
+      run<25>("v_add_f32 dep chain", 8, w);
+    }
+    return 0;
+  }
   for (int w : {1, 4, 6, 8}) {
     run<0>("v_pk_max_i16 x8 indep", 8, w);
     run<1>("v_pk_sub_u16 clamp x8", 8, w);
