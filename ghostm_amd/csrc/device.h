@@ -121,7 +121,8 @@ class DeviceModule {
 
  private:
   DeviceModule() = default;
-  void LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, const DevDb *d);
+  // span: runs of slots whose hits may pair (a name group's slots)
+  void LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, const DevDb *d, uint32_t span);
   int device_ = -1;
   void *stream_ = nullptr;
   DeviceTimes times_;

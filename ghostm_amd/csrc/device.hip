@@ -111,7 +111,7 @@ struct DeviceModule::Impl {
   DevBuf tasks, score_out, end_out, guard_list;
   // K3 work (tb_sort: two histograms + total, two cursor arrays)
   DevBuf tb_qid, tb_end, tb_start, tb_ml;
-  DevBuf tb_width, tb_ncols, tb_key, tb_order1, tb_order2, tb_sort;
+  DevBuf tb_width, tb_ncols, tb_key, tb_order1, tb_order2, tb_sort, tb_pair_a, tb_pair_b;
   int cus = 256;
   // K4 work
   DevBuf keys, sel_count, sel_cand, sel_sid, slot_hits;
@@ -662,7 +662,7 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
 
 // K3 launch: the key formulation when its field widths hold (len < 511,
 // matches < 128, |h| < 8192), else the int32 kernel. GHOSTM_K3=int32 forces it.
-void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, const DevDb *d) {
+void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, const DevDb *d, uint32_t pair_span) {
   const uint32_t rows = q->L;
   Impl &I = *impl_;
   const Layout lay = ChooseLayout(rows, a.base);
@@ -701,6 +701,8 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
     I.tb_key.Reserve((size_t)n * 4);
     I.tb_order1.Reserve((size_t)n * 4);
     I.tb_order2.Reserve((size_t)n * 4);
+    I.tb_pair_a.Reserve((size_t)n * 4);
+    I.tb_pair_b.Reserve((size_t)n * 4);
     I.tb_sort.Reserve((size_t)(4 * NB + 2) * 4);
     uint32_t *hist1 = I.tb_sort.as<uint32_t>(), *hist2 = hist1 + NB + 1;
     uint32_t *cur1 = hist2 + NB + 1, *cur2 = cur1 + NB;
@@ -709,7 +711,13 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
     const uint32_t *subj = d && d->nsubj ? d->subj.as<uint32_t>() : nullptr;
     hipLaunchKernelGGL(kern::k_tb_prep, g256, b256, 0, S(stream_), a.qid, a.end, n, a.base, subj,
                        subj ? d->nsubj : 0u, d ? d->len : 0u, I.tb_width.as<uint32_t>(),
-                       I.tb_ncols.as<uint32_t>(), I.tb_key.as<uint32_t>(), hist1, hist2);  // empty -> hist2[0]
+                       I.tb_ncols.as<uint32_t>(), hist2);  // empty slots -> hist2[0]
+    const uint32_t ps = std::max<uint32_t>(pair_span, 1);
+    const uint32_t runs_per_span = (ps + kern::kPairRun - 1) / kern::kPairRun;
+    const uint64_t runs = (uint64_t)((n + ps - 1) / ps) * runs_per_span;
+    hipLaunchKernelGGL(kern::k_tb_pairs, dim3((uint32_t)((runs + 255) / 256)), b256, 0, S(stream_), a.qid,
+                       I.tb_width.as<uint32_t>(), n, ps, I.tb_pair_a.as<uint32_t>(), I.tb_pair_b.as<uint32_t>(),
+                       I.tb_key.as<uint32_t>(), hist1);
     hipLaunchKernelGGL(kern::k_csort_scatter, g256, b256, 0, S(stream_), I.tb_key.as<uint32_t>(), n, true,
                        hist1, cur1, I.tb_order1.as<uint32_t>());
     kern::TbScanArgs sa{};
@@ -723,6 +731,8 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
     sa.qid = a.qid;
     sa.end = a.end;
     sa.width = I.tb_width.as<uint32_t>();
+    sa.pair_a = I.tb_pair_a.as<uint32_t>();
+    sa.pair_b = I.tb_pair_b.as<uint32_t>();
     sa.key = I.tb_key.as<uint32_t>();
     if (q->rcodes_lpad != lay.Lpad) {
       q->rcodes.Reserve((size_t)q->nseq * lay.Lpad + 16);
@@ -847,7 +857,7 @@ void DeviceModule::MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, 
   HIP_CHECK(hipMemsetAsync(I.counters.p, 0, 24, S(stream_)));
   a.cells = I.counters.as<unsigned long long>() + 1;
   HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
-  LaunchTraceback(a, q, (uint32_t)slots, d);
+  LaunchTraceback(a, q, (uint32_t)slots, d, cap);
   HIP_CHECK(hipEventRecord(I.ev1, S(stream_)));
   hipLaunchKernelGGL(kern::k_finalize, dim3((uint32_t)((slots + 255) / 256)), dim3(256), 0, S(stream_),
                      I.sel_count.as<uint32_t>(), I.sel_cand.as<uint32_t>(), I.sel_sid.as<uint32_t>(),
@@ -958,7 +968,7 @@ void DeviceModule::TraceBack(DevQuery *q, DevDb *d, uint32_t n, const uint32_t *
   HIP_CHECK(hipMemsetAsync(I.counters.p, 0, 24, S(stream_)));
   a.cells = I.counters.as<unsigned long long>() + 1;
   HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
-  LaunchTraceback(a, q, n, d);
+  LaunchTraceback(a, q, n, d, kern::kPairRun);
   HIP_CHECK(hipEventRecord(I.ev1, S(stream_)));
   std::vector<uint32_t> ml(n);
   HIP_CHECK(hipMemcpyAsync(db_start, I.tb_start.p, (size_t)n * 4, hipMemcpyDeviceToHost, S(stream_)));

@@ -1385,58 +1385,100 @@ __global__ void k_records(const uint32_t *sel_count, const SlotHit *slots, const
 // scores-only pass costs about a third of the key DP per column.
 //
 // Work is balanced by sorting: k_tb_prep computes each hit's reverse window
-// (the reverse scan stops at the subject's first residue: aligner.cpp:801-812)
-// and pairs hits of one query; k_csort_scatter orders the pairs by width for
+// (the reverse scan stops at the subject's first residue: aligner.cpp:801-812),
+// k_tb_pairs pairs hits of one query by window; k_csort_scatter orders the pairs by width for
 // k_tb_scan and the hits by j* + 1 for the key kernel, so each wave's lane
 // groups run windows of about the same length.
 constexpr uint32_t kSortBins = 1024;   // counting-sort keys (column counts), clamped
 constexpr int kScanBlock = 1024;       // one workgroup per CU: the pair table fills the LDS
 constexpr uint32_t kPairCodes = 26;    // DB codes 0..25 (25 = END) index the pair table
 
-// Per slot: the reverse window (0 = empty slot; counted into *empty), ncols reset to 0; per item
-// (= its first slot): the pair key, counted into hist[key] and hist[kSortBins]
-// (total). A pair is slots (2m, 2m+1) of the same query; an odd slot whose
-// query equals its even neighbour's belongs to that pair and is no item.
+// Per slot: the reverse window (0 = empty slot; counted into *empty), ncols
+// reset to 0.
 __global__ __launch_bounds__(256) void k_tb_prep(const uint32_t *qid, const uint32_t *end, uint32_t n,
                                                  uint32_t base, const uint32_t *subj, uint32_t nsubj,
                                                  uint32_t dblen, uint32_t *width, uint32_t *ncols,
-                                                 uint32_t *key, uint32_t *hist, uint32_t *empty) {
-  __shared__ uint32_t s_hist[kSortBins];
-  __shared__ uint32_t s_total, s_empty;
-  for (uint32_t b = threadIdx.x; b < kSortBins; b += blockDim.x) s_hist[b] = 0;
-  if (threadIdx.x == 0) { s_total = 0; s_empty = 0; }
+                                                 uint32_t *empty) {
+  __shared__ uint32_t s_empty;
+  if (threadIdx.x == 0) s_empty = 0;
   __syncthreads();
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  auto window = [&](uint32_t s) -> uint32_t {
-    if (qid[s] == 0xFFFFFFFFu) return 0;
-    const uint32_t p0 = end[s];
-    uint32_t w = p0 < base ? p0 + 1 : base;
-    if (nsubj) {
-      const uint32_t sid = SubjectOf(subj, nsubj, dblen, p0);
-      if (sid != 0xFFFFFFFFu) w = min(w, p0 - subj[sid] + 1);
-    }
-    return w;
-  };
   if (k < n) {
-    const uint32_t w = window(k);
+    uint32_t w = 0;
+    if (qid[k] != 0xFFFFFFFFu) {
+      const uint32_t p0 = end[k];
+      w = p0 < base ? p0 + 1 : base;
+      if (nsubj) {
+        const uint32_t sid = SubjectOf(subj, nsubj, dblen, p0);
+        if (sid != 0xFFFFFFFFu) w = min(w, p0 - subj[sid] + 1);
+      }
+    }
     width[k] = w;
     ncols[k] = 0;
     if (!w) atomicAdd(&s_empty, 1u);
-    const uint32_t q = qid[k];
-    uint32_t item = w;
-    if (w && (k & 1) && qid[k - 1] == q) item = 0;           // the even slot's partner
-    if (w && !(k & 1) && k + 1 < n && qid[k + 1] == q) item = max(w, window(k + 1));
-    key[k] = min(item, kSortBins - 1);
-    if (item) {
-      atomicAdd(&s_hist[min(item, kSortBins - 1)], 1u);
-      atomicAdd(&s_total, 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && s_empty) atomicAdd(empty, s_empty);
+}
+
+// Pairs for k_tb_scan: within each run of `span` slots (a name group's slots),
+// hits of one query sorted by window and paired neighbour with neighbour, so a
+// pair's two halves scan about the same number of columns. Item m of the run
+// (pair_a/pair_b at run start + m; pair_b = none for a single) gets key = the
+// longer window, counted into hist[key] and hist[kSortBins] (total); unused
+// item positions get key 0.
+constexpr uint32_t kPairRun = 32;  // longer runs are paired 32 slots at a time
+__global__ __launch_bounds__(256) void k_tb_pairs(const uint32_t *qid, const uint32_t *width, uint32_t n,
+                                                  uint32_t span, uint32_t *pair_a, uint32_t *pair_b,
+                                                  uint32_t *key, uint32_t *hist) {
+  __shared__ uint32_t s_hist[kSortBins];
+  __shared__ uint32_t s_total;
+  for (uint32_t b = threadIdx.x; b < kSortBins; b += blockDim.x) s_hist[b] = 0;
+  if (threadIdx.x == 0) s_total = 0;
+  __syncthreads();
+  const uint32_t runs_per_span = (span + kPairRun - 1) / kPairRun;
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t span_id = r / runs_per_span, sub = r - span_id * runs_per_span;
+  const uint64_t first64 = (uint64_t)span_id * span + (uint64_t)sub * kPairRun;
+  if (first64 < n && sub * kPairRun < span) {
+    const uint32_t first = (uint32_t)first64;
+    const uint32_t len = min(min(kPairRun, span - sub * kPairRun), n - first);
+    // (qid, width, slot) ascending; empty slots (width 0) left out
+    unsigned long long e[kPairRun];
+    uint32_t m = 0;
+    for (uint32_t k = 0; k < len; ++k) {
+      const uint32_t w = width[first + k];
+      if (!w) continue;
+      const unsigned long long v = (unsigned long long)qid[first + k] << 32 | (unsigned long long)w << 16 | k;
+      uint32_t at = m++;
+      while (at > 0 && e[at - 1] > v) { e[at] = e[at - 1]; --at; }
+      e[at] = v;
     }
+    uint32_t items = 0;
+    for (uint32_t k = 0; k < m;) {
+      const uint32_t a = first + (uint32_t)(e[k] & 0xFFFFu), wa = (uint32_t)(e[k] >> 16) & 0xFFFFu;
+      uint32_t b = 0xFFFFFFFFu, wb = 0;
+      if (k + 1 < m && (e[k] >> 32) == (e[k + 1] >> 32)) {
+        b = first + (uint32_t)(e[k + 1] & 0xFFFFu);
+        wb = (uint32_t)(e[k + 1] >> 16) & 0xFFFFu;
+        k += 2;
+      } else {
+        k += 1;
+      }
+      const uint32_t kk = min(max(wa, wb), kSortBins - 1);
+      pair_a[first + items] = a;
+      pair_b[first + items] = b;
+      key[first + items] = kk;
+      ++items;
+      atomicAdd(&s_hist[kk], 1u);
+    }
+    for (uint32_t k = items; k < len; ++k) key[first + k] = 0;
+    if (items) atomicAdd(&s_total, items);
   }
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < kSortBins; b += blockDim.x)
     if (s_hist[b]) atomicAdd(&hist[b], s_hist[b]);
   if (threadIdx.x == 0 && s_total) atomicAdd(&hist[kSortBins], s_total);
-  if (threadIdx.x == 0 && s_empty) atomicAdd(empty, s_empty);
 }
 
 // Counting-sort scatter: order[prefix(key) + rank] = index, for every index with
@@ -1494,7 +1536,7 @@ struct TbScanArgs {
   const int *mat;              // 32x32 substitution matrix (row = DB code)
   const uint32_t *qid, *end;   // per slot
   const uint32_t *width;       // per slot, from k_tb_prep
-  const uint32_t *key;         // per item (its first slot), from k_tb_prep
+  const uint32_t *pair_a, *pair_b, *key;  // per item, from k_tb_pairs
   const uint32_t *rcodes;      // k_rev_codes: per query Lpad/4 words of row code offsets
   uint32_t n, base;            // slots; reverse window limit
   const uint32_t *items;       // pair items sorted by width; count in item_total[0]
@@ -1548,12 +1590,13 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
     const uint32_t it = first + g;
     uint32_t sA = 0xFFFFFFFFu, sB = 0xFFFFFFFFu, wA = 0, wB = 0, p0A = 0, p0B = 0, q = 0;
     if (g < a.gpw && it < nitems) {
-      sA = a.items[it];
+      const uint32_t item = a.items[it];
+      sA = a.pair_a[item];
+      sB = a.pair_b[item];
       q = a.qid[sA];
       wA = a.width[sA];
       p0A = a.end[sA];
-      if (!(sA & 1) && sA + 1 < a.n && a.qid[sA + 1] == q && a.width[sA + 1]) {
-        sB = sA + 1;
+      if (sB != 0xFFFFFFFFu) {
         wB = a.width[sB];
         p0B = a.end[sB];
       }
@@ -1588,10 +1631,10 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
     // items ascend by key = max(wA, wB): the batch's last item has the longest
     // window (a clamped key stands for the whole window)
     const uint32_t last = a.items[min(first + a.gpw, nitems) - 1];
-    uint32_t wmax = __builtin_amdgcn_readfirstlane(a.key[last]);
+    uint32_t wmax = __builtin_amdgcn_readfirstlane(a.key[last]);  // key of an item index
     if (wmax >= kSortBins - 1) wmax = a.base;
     const uint32_t steps = wmax + a.G - 1;
-    // residues of the reverse window, one column ahead; outside the window (fill:
+    // residues of the reverse window, two columns ahead; outside the window (fill:
     // j < 0, beyond: its end or the subject's start) a column behaves as END.
     // The load address stays inside the window (p0 itself when outside).
     auto fetch = [&](int jj, uint32_t p0, uint32_t w) -> uint32_t {
@@ -1599,15 +1642,18 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
       const uint32_t x = a.db[p0 - (in ? (uint32_t)jj : 0u)];
       return in ? x : kSeqEnd;
     };
-    uint32_t nA = fetch(j, p0A, wA), nB = fetch(j, p0B, wB);
+    uint32_t nA = fetch(j, p0A, wA), nB = fetch(j, p0B, wB);             // this column
+    uint32_t mA = fetch(j + 1, p0A, wA), mB = fetch(j + 1, p0B, wB);     // the next one
     for (uint32_t step = 0; step < steps; ++step, ++j) {
       uint32_t hin = ShiftUp(hout), fin = ShiftUp(fout);
       if (i == 0) { hin = 0; fin = 0; }
       const uint32_t diag0 = hprev;
       hprev = hin;
       const uint32_t rA = nA, rB = nB;
-      nA = fetch(j + 1, p0A, wA);
-      nB = fetch(j + 1, p0B, wB);
+      nA = mA;
+      nB = mB;
+      mA = fetch(j + 2, p0A, wA);
+      mB = fetch(j + 2, p0B, wB);
       const uint32_t end = (rA == kSeqEnd ? 0x0000FFFFu : 0u) | (rB == kSeqEnd ? 0xFFFF0000u : 0u);
       if (j >= 0) dead |= end;                  // the reference breaks at END
       const typename C::Step st = cell.At(end, prev_end);
