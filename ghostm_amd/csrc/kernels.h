@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "libstdcxx_sort.h"
 
 namespace ghostm {
@@ -736,6 +738,31 @@ __device__ inline uint32_t ShiftUp(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xF, 0xF, true);  // bound_ctrl: lane 0 reads 0
 }
 
+// Bitwise/packed helpers as single instructions: written in C the compiler
+// turns these mask selects into compare + v_cndmask pairs per half.
+__device__ inline uint32_t BfiV(uint32_t m, uint32_t x, uint32_t y) {  // (x & m) | (y & ~m)
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(x), "v"(y));
+  return r;
+}
+__device__ inline uint32_t PkAddU16(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_pk_add_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ inline uint32_t PkSubI16(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_pk_sub_i16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ inline uint32_t PkSign(uint32_t a) {  // 0xFFFF in each negative half
+  uint32_t r;
+  // op_sel_hi:[0,1]: the high lane takes the shift count from the constant's low
+  // half too (an inline constant's high half is 0)
+  asm("v_pk_ashrrev_i16 %0, 15, %1 op_sel_hi:[0,1]" : "=v"(r) : "v"(a));
+  return r;
+}
+
 // Packed cell arithmetic of the two encodings. Scores of both encodings are
 // non-negative, so their 16-bit patterns order like their values.
 //
@@ -784,7 +811,7 @@ template <> struct Cells<true> {
   }
   __device__ Cells(int open, int ext) : nopen(Pair(open)), next(Pair(ext)) {}
   __device__ Step At(uint32_t end, uint32_t prev_end) const {
-    return Step{HF((nopen & ~end) | (kBig & end)), HF((next & ~end) | (kBig & end)), HF(kOne & ~prev_end)};
+    return Step{HF(BfiV(end, kBig, nopen)), HF(BfiV(end, kBig, next)), HF(kOne & ~prev_end)};
   }
   __device__ static uint32_t Diag(uint32_t h, hf2 m, uint32_t p) {
     return W(__builtin_elementwise_fma(HF(h), m, HF(p)));
@@ -794,8 +821,9 @@ template <> struct Cells<true> {
     const hf2 h = __builtin_elementwise_maximum(__builtin_elementwise_maximum(HF(s), HF(E)), HF(F));
     H = W(h);
     const hf2 o = h + st.nopen;
-    E = W(__builtin_elementwise_maximum(__builtin_elementwise_maximum(HF(E) + st.next, o), zero));
+    // F first: the next row's max3 reads it, and E's update then sits between
     F = W(__builtin_elementwise_maximum(__builtin_elementwise_maximum(HF(F) + st.next, o), zero));
+    E = W(__builtin_elementwise_maximum(__builtin_elementwise_maximum(HF(E) + st.next, o), zero));
   }
   __device__ static uint32_t Max3(uint32_t a, uint32_t b, uint32_t c) {
     return W(__builtin_elementwise_maximum(__builtin_elementwise_maximum(HF(a), HF(b)), HF(c)));
@@ -805,6 +833,12 @@ template <> struct Cells<true> {
     return (int)(float)__builtin_bit_cast(_Float16, (unsigned short)bits16);
   }
 };
+
+__device__ inline uint32_t MadU24(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
 
 __device__ inline uint32_t MulU24(uint32_t a, uint32_t b) {
   uint32_t r;
@@ -858,10 +892,16 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16(ScoreArgs a) {
   // element index of profile row 0 of this lane's rows; row c is + c * RS
   const uint32_t baseA = slotA * kProfRows16 * RS + i * S;
   const uint32_t baseB = slotB * kProfRows16 * RS + i * S;
-  // DB residues are padded with END on both sides (kDbFrontPad in front): the
-  // column loads below need no bounds test, the window test picks END
+  // DB residues are padded with END on both sides (kDbFrontPad in front, 64 KiB
+  // behind): the column loads need no bounds test. An empty half reads the back
+  // padding, and a window cut by the DB's end (width < base) reads END past it,
+  // so inside the main loop (every lane's column in [0, base)) no window test is
+  // needed; only the fill (j < 0) and drain (j >= base) steps test.
   const uint8_t *dbp = a.db - kDbFrontPad;
-  const uint32_t xA = offA + kDbFrontPad, xB = offB + kDbFrontPad;
+  const uint32_t back = kDbFrontPad + a.dblen;
+  const uint32_t xA = (vA ? offA + kDbFrontPad : back) - i, xB = (vB ? offB + kDbFrontPad : back) - i;
+  const uint32_t RS2 = RS * 2;                               // profile row stride, bytes
+  const uint32_t baseA2 = baseA * 2, baseB2 = baseB * 2;
   const C cell(a.open, a.ext);
 
   uint32_t H[S], E[S];
@@ -869,37 +909,46 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16(ScoreArgs a) {
   for (int k = 0; k < S; ++k) { H[k] = 0; E[k] = 0; }
   uint32_t best = 0;                     // packed best column max (16-bit patterns)
   uint32_t col = 0;                      // packed column of the last best (>=)
-  uint32_t ncols = 0;                    // packed count of non-END columns
+  uint32_t jj = ((0u - i) & 0xFFFFu) * 0x10001u;  // this lane's column j in both halves (packed, mod 2^16)
+  uint32_t nend = 0;                     // packed count of END columns, as -count (mod 2^16)
   uint32_t hout = 0, fout = 0, hprev = 0;
   uint32_t prev_end = 0xFFFFFFFFu;       // the column before the first one: nothing to carry
-  int j = -(int)i;
-  // residues two deep: n* = this column's (window-tested), x* = next column's raw
-  uint32_t nA = dbp[xA + j], nB = dbp[xB + j];
-  nA = (uint32_t)j < wA ? nA : kSeqEnd;
-  nB = (uint32_t)j < wB ? nB : kSeqEnd;
-  uint32_t pxA = dbp[xA + (uint32_t)(j + 1)], pxB = dbp[xB + (uint32_t)(j + 1)];
+  // raw residues two deep: c0* = this column's, c1* = the next one's; the
+  // address is a uniform column base (dbp + step) plus the lane's offset x - i
+  uint32_t c0A = dbp[xA], c0B = dbp[xB], c1A = dbp[xA + 1], c1B = dbp[xB + 1];
   const uint32_t steps = a.base + a.G - 1;
-  for (uint32_t step = 0; step < steps; ++step, ++j) {
+  const uint32_t wA_ = vA ? wA : 0u, wB_ = vB ? wB : 0u;
+  auto column = [&](uint32_t step, auto tested_c) {
+    constexpr bool tested = decltype(tested_c)::value;
     uint32_t hin = ShiftUp(hout), fin = ShiftUp(fout);
     if (i == 0) { hin = 0; fin = 0; }
     const uint32_t diag0 = hprev;
     hprev = hin;
-    const uint32_t rA = nA, rB = nB;
-    nA = (uint32_t)(j + 1) < wA ? pxA : kSeqEnd;
-    nB = (uint32_t)(j + 1) < wB ? pxB : kSeqEnd;
-    pxA = dbp[xA + (uint32_t)(j + 2)];
-    pxB = dbp[xB + (uint32_t)(j + 2)];
-    // inactive columns (fill, drain, beyond the window) behave as END
-    const uint32_t end = (rA == kSeqEnd ? 0x0000FFFFu : 0u) | (rB == kSeqEnd ? 0xFFFF0000u : 0u);
+    uint32_t rA = c0A, rB = c0B;
+    if constexpr (tested) {
+      // fill (j < 0) and drain (j >= width) columns behave as END
+      const uint32_t j = step - i;
+      rA = j < wA_ ? rA : kSeqEnd;
+      rB = j < wB_ ? rB : kSeqEnd;
+    }
+    c0A = c1A;
+    c0B = c1B;
+    const uint8_t *colp = dbp + step + 2;
+    c1A = colp[xA];
+    c1B = colp[xB];
+    // END halves: codes are 0..25 with END = 25 the largest, so code + 0x7FE7
+    // reaches bit 15 only for END (packed add, then an arithmetic shift)
+    const uint32_t rr = rA | (rB << 16);
+    const uint32_t end = PkSign(PkAddU16(rr, 0x7FE77FE7u));
     const typename C::Step st = cell.At(end, prev_end);
     prev_end = end;
-    const short *pA = s_prof16 + (baseA + MulU24(rA, RS));
-    const short *pB = s_prof16 + (baseB + MulU24(rB, RS));
+    const char *pA = reinterpret_cast<const char *>(s_prof16) + MadU24(rA, RS2, baseA2);
+    const char *pB = reinterpret_cast<const char *>(s_prof16) + MadU24(rB, RS2, baseB2);
     uint32_t diag = diag0, F = fin, cm = 0;
 #pragma unroll
     for (int k = 0; k < S; k += 8) {
-      const uint4 qa = *reinterpret_cast<const uint4 *>(pA + k);
-      const uint4 qb = *reinterpret_cast<const uint4 *>(pB + k);
+      const uint4 qa = *reinterpret_cast<const uint4 *>(pA + 2 * k);
+      const uint4 qb = *reinterpret_cast<const uint4 *>(pB + 2 * k);
       const uint32_t wa[4] = {qa.x, qa.y, qa.z, qa.w}, wb[4] = {qb.x, qb.y, qb.z, qb.w};
       // diagonal sums of the chunk first, from the previous column's H, so the
       // row updates below overwrite H in place (no register rotation copies)
@@ -926,13 +975,20 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16(ScoreArgs a) {
     fout = F;
     // per half: the last column whose max reaches the best (>=), END columns
     // excluded. Patterns are < 0x8000, so cm - best is negative iff cm < best.
-    {
-      const uint32_t keep = W((S2(cm) - S2(best)) >> (short)15) | end;
-      best = (best & keep) | (cm & ~keep);
-      col = (col & keep) | (MulU24((uint32_t)j & 0xFFFFu, 0x10001u) & ~keep);  // j in both halves
-      ncols += 0x00010001u & ~end;
-    }
-  }
+    const uint32_t keep = PkSign(PkSubI16(cm, best)) | end;
+    best = BfiV(keep, best, cm);
+    col = BfiV(keep, col, jj);
+    jj = PkAddU16(jj, 0x00010001u);      // packed: no carry between the halves
+    nend = PkAddU16(nend, end);          // END halves add -1
+  };
+  const uint32_t fill = min(a.G - 1, steps);
+  uint32_t step = 0;
+  for (; step < fill; ++step) column(step, std::true_type{});
+  for (; step < a.base; ++step) column(step, std::false_type{});
+  for (; step < steps; ++step) column(step, std::true_type{});
+  // non-END columns per half: steps minus the END count
+  const uint32_t ncolsA = steps - ((0x10000u - (nend & 0xFFFFu)) & 0xFFFFu);
+  const uint32_t ncolsB = steps - ((0x10000u - (nend >> 16)) & 0xFFFFu);
   int BA = C::Decode(best & 0xFFFFu), CA = (int)(col & 0xFFFFu);
   int BB = C::Decode(best >> 16), CB = (int)(col >> 16);
   for (uint32_t k = 1; k < a.G; ++k) {
@@ -966,7 +1022,7 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16(ScoreArgs a) {
       }
     }
   }
-  WaveAddCells(a.cells, (in_group && i == 0) ? (unsigned long long)((ncols & 0xFFFFu) + (ncols >> 16)) * a.L
+  WaveAddCells(a.cells, (in_group && i == 0) ? (unsigned long long)((vA ? ncolsA : 0u) + (vB ? ncolsB : 0u)) * a.L
                                              : 0ull);
 }
 

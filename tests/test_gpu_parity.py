@@ -97,11 +97,13 @@ def _blosum62():
     return cases.parse_ncbi_matrix(os.path.join(cases.GOLDEN, "matrices", "BLOSUM62"))
 
 
-def test_reference_abi_stages_match_oracle(dataset, tmp_path):
+@pytest.mark.parametrize("ds", ["syn_small", "readme_kat"])
+def test_reference_abi_stages_match_oracle(ds, dataset, tmp_path):
     """InitGpu/SetOptionGpu/SetQueryGpu/SetDbGpu/SearchNextGpu/CalculateScoreGpu in
     the order the reference aligner.cpp drives them, then TraceBackGpu, compared
-    with the oracle's per-candidate (start, score, end) and traceback dumps."""
-    d = dataset("syn_small")
+    with the oracle's per-candidate (start, score, end) and traceback dumps.
+    readme_kat (L = 25) runs the one-lane-per-candidate layout (G = 1)."""
+    d = dataset(ds)
     prefix = str(tmp_path / "dump")
     cases.run_aln(cases.ORACLE, d, ["-y", "1"], {"GHOSTM_ORACLE_DUMP": prefix}, str(tmp_path / "o"))
     cand = np.fromfile(prefix + ".cand", dtype="<u4").reshape(-1, 4)
