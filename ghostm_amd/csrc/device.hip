@@ -111,7 +111,7 @@ struct DeviceModule::Impl {
   DevBuf tasks, score_out, end_out, guard_list;
   // K3 work (tb_sort: two histograms + total, two cursor arrays)
   DevBuf tb_qid, tb_end, tb_start, tb_ml;
-  DevBuf tb_width, tb_ncols, tb_key, tb_order1, tb_order2, tb_sort, tb_pair_a, tb_pair_b;
+  DevBuf tb_width, tb_ncols, tb_key, tb_order1, tb_order2, tb_sort, tb_pair_a, tb_pair_b, tb_best;
   int cus = 256;
   // K4 work
   DevBuf keys, sel_count, sel_cand, sel_sid, slot_hits;
@@ -147,11 +147,13 @@ void DeviceModule::Bind(int device) {
   HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_seed<512, 8192, false>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 8192 * 4));
   const int scan_lds = (int)kScanLds;
-#define GHOSTM_SCAN_ATTR(SS, HH)                                                                       \
-  HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_tb_scan<SS, HH>,                                 \
+#define GHOSTM_SCAN_ATTR(SS, HH, EE)                                                 \
+  HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_tb_scan<SS, HH, EE>,           \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, scan_lds));
-  GHOSTM_SCAN_ATTR(32, true) GHOSTM_SCAN_ATTR(32, false) GHOSTM_SCAN_ATTR(16, true)
-  GHOSTM_SCAN_ATTR(16, false) GHOSTM_SCAN_ATTR(8, true) GHOSTM_SCAN_ATTR(8, false)
+#define GHOSTM_SCAN_ATTR2(SS, HH) GHOSTM_SCAN_ATTR(SS, HH, true) GHOSTM_SCAN_ATTR(SS, HH, false)
+  GHOSTM_SCAN_ATTR2(32, true) GHOSTM_SCAN_ATTR2(32, false) GHOSTM_SCAN_ATTR2(16, true)
+  GHOSTM_SCAN_ATTR2(16, false) GHOSTM_SCAN_ATTR2(8, true) GHOSTM_SCAN_ATTR2(8, false)
+#undef GHOSTM_SCAN_ATTR2
 #undef GHOSTM_SCAN_ATTR
   {
     hipDeviceProp_t p;
@@ -684,6 +686,7 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
   if (key) a.mat_tb = I.mat_tbk.as<int>() + (key17 ? 32 * 32 : 0);
   a.order = nullptr;
   a.ncols = nullptr;
+  a.best_h = nullptr;
   // Two-pass traceback (kernels.h K3a): a scores-only reverse scan finds each
   // hit's first maximal column j*, then the traceback DP runs columns 0..j*
   // only, hits sorted by that count. Needs the packed encodings' value range
@@ -703,6 +706,7 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
     I.tb_order2.Reserve((size_t)n * 4);
     I.tb_pair_a.Reserve((size_t)n * 4);
     I.tb_pair_b.Reserve((size_t)n * 4);
+    I.tb_best.Reserve((size_t)n * 4);
     I.tb_sort.Reserve((size_t)(4 * NB + 2) * 4);
     uint32_t *hist1 = I.tb_sort.as<uint32_t>(), *hist2 = hist1 + NB + 1;
     uint32_t *cur1 = hist2 + NB + 1, *cur2 = cur1 + NB;
@@ -756,29 +760,39 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
     const uint32_t pairs_per_block = (kern::kScanBlock / 64) * lay.gpw;
     const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)I.cus,
                                                                      (n + pairs_per_block - 1) / pairs_per_block));
-#define GHOSTM_SCAN(SS)                                                                                      \
-  if (half) hipLaunchKernelGGL((kern::k_tb_scan<SS, true>), dim3(blocks), dim3(kern::kScanBlock), kScanLds,   \
-                               S(stream_), sa);                                                              \
-  else hipLaunchKernelGGL((kern::k_tb_scan<SS, false>), dim3(blocks), dim3(kern::kScanBlock), kScanLds,       \
-                          S(stream_), sa);
+    // exact windows (cut at the subject's start) need the DB's subject table
+    const bool exact = subj != nullptr;
+    sa.best_out = I.tb_best.as<uint32_t>();
+#define GHOSTM_SCAN1(SS, HH, EE) \
+  hipLaunchKernelGGL((kern::k_tb_scan<SS, HH, EE>), dim3(blocks), dim3(kern::kScanBlock), kScanLds, S(stream_), sa)
+#define GHOSTM_SCAN(SS)                            \
+  if (half && exact) GHOSTM_SCAN1(SS, true, true); \
+  else if (half) GHOSTM_SCAN1(SS, true, false);    \
+  else if (exact) GHOSTM_SCAN1(SS, false, true);   \
+  else GHOSTM_SCAN1(SS, false, false);
     switch (lay.S) {
       case 32: GHOSTM_SCAN(32); break;
       case 16: GHOSTM_SCAN(16); break;
       default: GHOSTM_SCAN(8); break;
     }
 #undef GHOSTM_SCAN
+#undef GHOSTM_SCAN1
     hipLaunchKernelGGL(kern::k_csort_scatter, g256, b256, 0, S(stream_), I.tb_ncols.as<uint32_t>(), n, false,
                        hist2, cur2, I.tb_order2.as<uint32_t>());
     HIP_CHECK(hipGetLastError());
     a.order = I.tb_order2.as<uint32_t>();
     a.ncols = I.tb_ncols.as<uint32_t>();
+    a.best_h = I.tb_best.as<uint32_t>();
     times_.traceback_launches_scan += 1;
   }
   const uint32_t per_block = (kern::kTbBlock / 64) * lay.gpw;
   const dim3 grid((n + per_block - 1) / per_block), block(kern::kTbBlock);
-#define GHOSTM_TB(SS)                                                                        \
-  if (key16) hipLaunchKernelGGL((kern::k_traceback_key<SS, 16>), grid, block, 0, S(stream_), a); \
-  else if (key17) hipLaunchKernelGGL((kern::k_traceback_key<SS, 17>), grid, block, 0, S(stream_), a); \
+  const bool fin = a.best_h != nullptr;  // the scan's maxima: no running maximum in the key DP
+#define GHOSTM_TB(SS)                                                                                              \
+  if (key16 && fin) hipLaunchKernelGGL((kern::k_traceback_key<SS, 16, true>), grid, block, 0, S(stream_), a);      \
+  else if (key16) hipLaunchKernelGGL((kern::k_traceback_key<SS, 16, false>), grid, block, 0, S(stream_), a);       \
+  else if (key17 && fin) hipLaunchKernelGGL((kern::k_traceback_key<SS, 17, true>), grid, block, 0, S(stream_), a); \
+  else if (key17) hipLaunchKernelGGL((kern::k_traceback_key<SS, 17, false>), grid, block, 0, S(stream_), a);       \
   else hipLaunchKernelGGL(kern::k_traceback<SS>, grid, block, 0, S(stream_), a);
   switch (lay.S) {
     case 32: GHOSTM_TB(32); break;

@@ -1047,6 +1047,9 @@ struct TbArgs {
   // null = slot order, the whole window
   const uint32_t *order;
   const uint32_t *ncols;
+  // with ncols: each hit's maximum from the scan; the key kernel then keeps no
+  // running maximum and reads the first maximal cell off column j* at the end
+  const uint32_t *best_h;
 };
 
 // the wave's largest value (loop bound of a lane-group loop)
@@ -1194,7 +1197,7 @@ __device__ inline uint32_t Bfi(uint32_t m, uint32_t x, uint32_t y) {
 
 __device__ inline int ShiftUpI(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xF, 0xF, false); }
 
-template <int S, int MLW>
+template <int S, int MLW, bool FINAL>
 __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
   using KL = KeyLayout<MLW>;
   __shared__ int s_key[32 * 32];
@@ -1285,10 +1288,12 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
           // strict > on h: above the ml field sit h << 2 and the cleared prio
           // (MLW 16: one SDWA compare of the high words; otherwise kc > bestK | kMl,
           // the same test as floor(kc / 2^MLW) > floor(bestK / 2^MLW))
-          bool better;
-          if constexpr (MLW == 16) better = (kc >> MLW) > (bestK >> MLW);
-          else better = kc > (int)((uint32_t)bestK | KL::kMl);
-          if (better) { bestK = kc; best_col = j; }
+          if constexpr (!FINAL) {
+            bool better;
+            if constexpr (MLW == 16) better = (kc >> MLW) > (bestK >> MLW);
+            else better = kc > (int)((uint32_t)bestK | KL::kMl);
+            if (better) { bestK = kc; best_col = j; }
+          }
         }
       }
       kout = K[S - 1];
@@ -1299,13 +1304,37 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
       kfout = 0;
     }
   }
-  // first cell (column-major, rows in processing order) reaching the maximum
-  int B = bestK >> KL::kHS, C = best_col, ML = (int)((uint32_t)bestK & KL::kMl);
-  for (uint32_t k = 1; k < a.G; ++k) {
-    const int src = (int)(g * a.G + k);
-    const int ok = __shfl(bestK, src), oc = __shfl(best_col, src);
-    const int ob = ok >> KL::kHS;
-    if (ob > B || (ob == B && ob > 0 && oc < C)) { B = ob; C = oc; ML = (int)((uint32_t)ok & KL::kMl); }
+  int C, ML;
+  if constexpr (FINAL) {
+    // K holds the lane's last column, j* = width - 1, where the hit's maximum
+    // first appears: the first maximal cell is the first row (processing order:
+    // lanes, then rows) there whose h equals it. A maximum of 0 keeps the
+    // reference's initial j* = 0 and empty (len, match).
+    const uint32_t bh = valid ? a.best_h[hit] : 0u;
+    int found = 0, fml = 0;
+    if (bh) {
+#pragma unroll
+      for (int u = S - 1; u >= 0; --u)
+        if (((uint32_t)K[u] >> KL::kHS) == bh) { found = 1; fml = (int)((uint32_t)K[u] & KL::kMl); }
+    }
+    for (uint32_t k = 1; k < a.G; ++k) {
+      const int src = (int)(g * a.G + k);
+      const int of = __shfl(found, src), om = __shfl(fml, src);
+      if (!found && of) { found = 1; fml = om; }
+    }
+    C = bh ? (int)width - 1 : 0;
+    ML = bh ? fml : 0;
+  } else {
+    // first cell (column-major, rows in processing order) reaching the maximum
+    int B = bestK >> KL::kHS;
+    C = best_col;
+    ML = (int)((uint32_t)bestK & KL::kMl);
+    for (uint32_t k = 1; k < a.G; ++k) {
+      const int src = (int)(g * a.G + k);
+      const int ok = __shfl(bestK, src), oc = __shfl(best_col, src);
+      const int ob = ok >> KL::kHS;
+      if (ob > B || (ob == B && ob > 0 && oc < C)) { B = ob; C = oc; ML = (int)((uint32_t)ok & KL::kMl); }
+    }
   }
   if (valid && i == 0) {
     a.out_start[hit] = p0 - (uint32_t)C;
@@ -1599,6 +1628,7 @@ struct TbScanArgs {
   const uint32_t *item_total;
   int open, ext;
   uint32_t *ncols;             // per slot: j* + 1
+  uint32_t *best_out;          // per slot: the reverse DP's maximum
   uint32_t *hist;              // histogram of ncols (kSortBins)
   unsigned long long *cells;   // += L x scanned columns
 };
@@ -1623,7 +1653,7 @@ __global__ void k_rev_codes(const uint8_t *qseq, uint32_t nq, uint32_t L, uint32
 // Pair table in LDS: word (a, b, q) = (M[a][q], M[b][q]) encoded in the two
 // halves; the byte offset ((a * 32 + b) << 7) + 4q is one SDWA add per row, and
 // one ds_read_b32 gives both hits' profile values, with no v_perm.
-template <int S, bool HALF>
+template <int S, bool HALF, bool EXACT>
 __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
   using C = Cells<HALF>;
   extern __shared__ __attribute__((aligned(16))) uint32_t s_pair[];
@@ -1683,24 +1713,33 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
     uint32_t best = 0, col = 0;                 // packed halves
     uint32_t dead = (wA ? 0u : 0x0000FFFFu) | (wB ? 0u : 0xFFFF0000u);
     uint32_t hout = 0, fout = 0, hprev = 0, prev_end = 0xFFFFFFFFu;
-    int j = -(int)i;
+    const uint32_t ww = wA | (wB << 16);                     // packed windows
+    uint32_t jj = ((0u - i) & 0xFFFFu) * 0x10001u;           // packed column j (mod 2^16)
+    const uint32_t clA = (wA ? wA : 1u) - 1, clB = (wB ? wB : 1u) - 1;
     // items ascend by key = max(wA, wB): the batch's last item has the longest
     // window (a clamped key stands for the whole window)
     const uint32_t last = a.items[min(first + a.gpw, nitems) - 1];
     uint32_t wmax = __builtin_amdgcn_readfirstlane(a.key[last]);  // key of an item index
     if (wmax >= kSortBins - 1) wmax = a.base;
     const uint32_t steps = wmax + a.G - 1;
-    // residues of the reverse window, two columns ahead; outside the window (fill:
-    // j < 0, beyond: its end or the subject's start) a column behaves as END.
-    // The load address stays inside the window (p0 itself when outside).
-    auto fetch = [&](int jj, uint32_t p0, uint32_t w) -> uint32_t {
-      const bool in = jj >= 0 && (uint32_t)jj < w;
-      const uint32_t x = a.db[p0 - (in ? (uint32_t)jj : 0u)];
+    // residues of the reverse window, two columns ahead. General steps: outside
+    // the window (fill: j < 0, beyond: its end or the subject's start) a column
+    // behaves as END and the load address stays inside the window. Run steps
+    // (EXACT windows, every lane past its first column): the raw residue at a
+    // clamped address; columns beyond a window compute values nothing reads and
+    // are left out of the maximum.
+    auto fetch = [&](int jn, uint32_t p0, uint32_t w) -> uint32_t {
+      const bool in = jn >= 0 && (uint32_t)jn < w;
+      const uint32_t x = a.db[p0 - (in ? (uint32_t)jn : 0u)];
       return in ? x : kSeqEnd;
     };
-    uint32_t nA = fetch(j, p0A, wA), nB = fetch(j, p0B, wB);             // this column
-    uint32_t mA = fetch(j + 1, p0A, wA), mB = fetch(j + 1, p0B, wB);     // the next one
-    for (uint32_t step = 0; step < steps; ++step, ++j) {
+    auto fetch_raw = [&](uint32_t jn, uint32_t p0, uint32_t cl) -> uint32_t { return a.db[p0 - min(jn, cl)]; };
+    uint32_t nA = fetch(-(int)i, p0A, wA), nB = fetch(-(int)i, p0B, wB);           // this column
+    uint32_t mA = fetch(1 - (int)i, p0A, wA), mB = fetch(1 - (int)i, p0B, wB);     // the next one
+    const typename C::Step st_run = cell.At(0u, 0u);  // no END in this column or the one before
+    auto column = [&](uint32_t step, auto run_c) {
+      constexpr bool run = decltype(run_c)::value;
+      const int j = (int)step - (int)i;
       uint32_t hin = ShiftUp(hout), fin = ShiftUp(fout);
       if (i == 0) { hin = 0; fin = 0; }
       const uint32_t diag0 = hprev;
@@ -1708,12 +1747,20 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
       const uint32_t rA = nA, rB = nB;
       nA = mA;
       nB = mB;
-      mA = fetch(j + 2, p0A, wA);
-      mB = fetch(j + 2, p0B, wB);
-      const uint32_t end = (rA == kSeqEnd ? 0x0000FFFFu : 0u) | (rB == kSeqEnd ? 0xFFFF0000u : 0u);
-      if (j >= 0) dead |= end;                  // the reference breaks at END
-      const typename C::Step st = cell.At(end, prev_end);
-      prev_end = end;
+      uint32_t end = 0;
+      typename C::Step st = st_run;
+      if constexpr (run) {
+        mA = fetch_raw((uint32_t)(j + 2), p0A, clA);
+        mB = fetch_raw((uint32_t)(j + 2), p0B, clB);
+      } else {
+        mA = fetch(j + 2, p0A, wA);
+        mB = fetch(j + 2, p0B, wB);
+        // END halves: codes are 0..25 with END = 25 the largest
+        end = PkSign(PkAddU16(rA | (rB << 16), 0x7FE77FE7u));
+        if (j >= 0) dead |= end;                  // the reference breaks at END
+        st = cell.At(end, prev_end);
+        prev_end = end;
+      }
       const uint32_t cbase = (min(rA, kPairCodes - 1) << 12) | (rB << 7);
       const char *tp = reinterpret_cast<const char *>(s_pair) + cbase;
       auto T = [&](int u) { return *reinterpret_cast<const uint32_t *>(tp + ((qoff[u >> 2] >> (8 * (u & 3))) & 0xFFu)); };
@@ -1736,11 +1783,21 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
       }
       hout = H[S - 1];
       fout = F;
-      // strict first maximum per live half: best - cm < 0 iff cm > best
-      const uint32_t upd = W((S2(best) - S2(cm)) >> (short)15) & ~(end | dead);
-      best = (best & ~upd) | (cm & upd);
-      col = (col & ~upd) | (((uint32_t)j & 0xFFFFu) * 0x10001u & upd);
-    }
+      // strict first maximum per live half: best - cm < 0 iff cm > best. Live:
+      // inside the window (j - w < 0) on run steps, else neither END nor dead
+      const uint32_t live = run ? PkSign(PkSubI16(jj, ww)) : ~(end | dead);
+      const uint32_t upd = PkSign(PkSubI16(best, cm)) & live;
+      best = BfiV(upd, cm, best);
+      col = BfiV(upd, jj, col);
+      jj = PkAddU16(jj, 0x00010001u);
+    };
+    // EXACT windows (cut at the subject's start) meet no END inside; the first
+    // G steps still hold the fill columns and each lane's first column
+    uint32_t step = 0;
+    const uint32_t general = EXACT ? min(a.G, steps) : steps;
+    for (; step < general; ++step) column(step, std::false_type{});
+    if constexpr (EXACT)
+      for (; step < steps; ++step) column(step, std::true_type{});
     int BA = C::Decode(best & 0xFFFFu), CA = (int)(col & 0xFFFFu);
     int BB = C::Decode(best >> 16), CB = (int)(col >> 16);
     // first column over the group's row strips
@@ -1753,9 +1810,11 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
     }
     if (i == 0 && wA) {
       a.ncols[sA] = (uint32_t)CA + 1;
+      a.best_out[sA] = (uint32_t)BA;
       atomicAdd(&s_hist[min((uint32_t)CA + 1, kSortBins - 1)], 1u);
       if (wB) {
         a.ncols[sB] = (uint32_t)CB + 1;
+        a.best_out[sB] = (uint32_t)BB;
         atomicAdd(&s_hist[min((uint32_t)CB + 1, kSortBins - 1)], 1u);
       }
     }
