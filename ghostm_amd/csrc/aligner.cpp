@@ -708,6 +708,8 @@ void Session::Run() {
   stats_.traceback_cells = dt.traceback_cells;
   stats_.traceback_launches_scan = dt.traceback_launches_scan;
   stats_.traceback_scan_cells = dt.traceback_scan_cells;
+  stats_.merge_launches = dt.merge_launches;
+  stats_.merge_launches_wave = dt.merge_launches_wave;
   for (size_t k = 0; k < used_parts_; ++k)
     for (const auto &h : parts_[k].hits) stats_.hits += h.size();
 }

@@ -848,7 +848,23 @@ void DeviceModule::MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, 
   m.tb_qid = I.tb_qid.as<uint32_t>();
   m.tb_end = I.tb_end.as<uint32_t>();
   HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
-  hipLaunchKernelGGL(kern::k_merge, dim3((ng + 255) / 256), dim3(256), 0, S(stream_), m);
+  // K4: one wave per name group (keys in LDS) for -b up to kMergeBest, else
+  // one thread per group; GHOSTM_K4=thread|wave forces one (tests)
+  bool wave = best >= 1 && best <= kern::kMergeBest;
+  if (const char *force = getenv("GHOSTM_K4")) {
+    if (!strcmp(force, "thread")) wave = false;
+    else if (!strcmp(force, "wave") && best >= 1 && best <= kern::kMergeBest) wave = true;
+  }
+  m.wave_cap = kern::kMergeCap;
+  if (const char *c = getenv("GHOSTM_K4_CAP"))  // tests: send smaller groups to the one-lane fallback
+    m.wave_cap = std::min<uint32_t>((uint32_t)strtoul(c, nullptr, 10), kern::kMergeCap);
+  if (wave)
+    hipLaunchKernelGGL(kern::k_merge_wave, dim3((ng + kern::kMergeWaves - 1) / kern::kMergeWaves),
+                       dim3(64 * kern::kMergeWaves), 0, S(stream_), m);
+  else
+    hipLaunchKernelGGL(kern::k_merge, dim3((ng + 255) / 256), dim3(256), 0, S(stream_), m);
+  times_.merge_launches += 1;
+  times_.merge_launches_wave += wave ? 1 : 0;
   HIP_CHECK(hipGetLastError());
   HIP_CHECK(hipEventRecord(I.ev1, S(stream_)));
   times_.merge += ElapsedMs(I.ev0, I.ev1) * 1e-3;

@@ -1363,6 +1363,7 @@ struct MergeArgs {
   uint32_t *sel_sid;                   // [ng*cap]
   uint32_t *tb_qid;                    // [ng*cap] K3 request (0xFFFFFFFF = empty)
   uint32_t *tb_end;                    // [ng*cap]
+  uint32_t wave_cap;                   // k_merge_wave: largest group kept in LDS (<= kMergeCap)
 };
 
 // DB::GetID (db.h:106-135), unsigned arithmetic as the reference.
@@ -1383,9 +1384,8 @@ struct ScoreDescending {
   }
 };
 
-__global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= a.ng) return;
+// One name group's selection on one thread (k_merge; k_merge_wave's fallback).
+__device__ inline void MergeGroup(const MergeArgs &a, uint32_t g) {
   const uint32_t q0 = a.group_first[g], q1 = a.group_last[g];
   const unsigned long long b = a.offsets[q0] - a.out_base;
   const unsigned long long n = a.offsets[q1] + a.counts[q1] - a.out_base - b;
@@ -1415,6 +1415,187 @@ __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
   }
   a.sel_count[g] = count;
   for (uint32_t k = count; k < a.cap; ++k) a.tb_qid[(size_t)g * a.cap + k] = 0xFFFFFFFFu;
+}
+
+__global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < a.ng) MergeGroup(a, g);
+}
+
+// k_merge_wave: k_merge's selection with one wave per name group, the group's
+// (score, index) keys in LDS, and each step of std::sort's introsort done by
+// the whole wave. __unguarded_partition (pivot p at first, scan [first+1,
+// last)) stops its left scan at elements not less than p and its right scan at
+// elements p is not less than, and swaps the k-th left stop with the k-th
+// right stop from the end (the pivot's own position is the last one) while the
+// first lies below the second. Every position is scanned once before a swap
+// can touch it, so both stop lists come from the partition's input: ballots
+// and prefix counts give all swaps at once, and the pairs are disjoint. The
+// cut is the first left stop past the swapped pairs, or the last swapped right
+// stop when the left scan reaches that first (tests/native/test_stdsort.cpp
+// restates it sequentially and pins it against std::sort). The final insertion
+// sort of a <= 16-element part is a stable sort (ranks); the heap-sort
+// fallback (depth limit) and groups above kMergeCap keys run on one lane as in
+// k_merge. The walk then takes up to 64 finalized keys at a time: subjects by
+// binary search in parallel, first occurrences by lane order.
+constexpr uint32_t kMergeCap = 1024;   // keys per wave in LDS
+constexpr uint32_t kMergeWaves = 4;    // groups per workgroup
+constexpr uint32_t kMergeBest = 64;    // largest -b k_merge_wave takes
+
+__device__ inline void WaveSync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ inline uint32_t WaveMinU(uint32_t v) {
+  for (int d = 32; d > 0; d >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, d));
+  return v;
+}
+
+struct MergeFrame {
+  uint32_t first, last;
+  int depth;
+};
+
+// __unguarded_partition(K + first + 1, K + last, K + first) by stop lists;
+// returns the cut (ls, rs: per-wave LDS scratch, 1-based)
+__device__ uint32_t WavePartition(unsigned long long *K, uint32_t first, uint32_t last, uint16_t *ls,
+                                  uint16_t *rs, uint32_t lane) {
+  const uint32_t P = (uint32_t)(K[first] >> 32);
+  const unsigned long long below = (1ull << lane) - 1;
+  uint32_t nl = 0, nr = 0;
+  for (uint32_t base = first; base < last; base += 64) {
+    const uint32_t x = base + lane;
+    const uint32_t sc = x < last ? (uint32_t)(K[x] >> 32) : 0u;
+    // less(u, v) = score(u) > score(v): a left stop has score <= P, a right stop >= P
+    const bool isL = x > first && x < last && sc <= P;
+    const bool isR = x < last && sc >= P;
+    const unsigned long long bl = __ballot(isL), br = __ballot(isR);
+    if (isL) ls[nl + 1 + __popcll(bl & below)] = (uint16_t)x;
+    if (isR) rs[nr + 1 + __popcll(br & below)] = (uint16_t)x;  // ascending
+    nl += __popcll(bl);
+    nr += __popcll(br);
+  }
+  WaveSync();
+  // the k-th right stop from the end is rs[nr + 1 - k]; pair k is swapped while
+  // ls[k] < rs[nr + 1 - k], and the first k failing it ends the partition
+  uint32_t kf = nl + 1;
+  for (uint32_t k = lane + 1; k <= nl; k += 64)
+    if (!(k <= nr && rs[nr + 1 - k] > ls[k])) kf = min(kf, k);
+  kf = WaveMinU(kf);
+  for (uint32_t k = lane + 1; k < kf; k += 64) {
+    const uint32_t x = ls[k], y = rs[nr + 1 - k];
+    const unsigned long long vx = K[x], vy = K[y];
+    K[x] = vy;
+    K[y] = vx;
+  }
+  WaveSync();
+  uint32_t cut = kf <= nl ? (uint32_t)ls[kf] : last;
+  if (kf >= 2) cut = min(cut, (uint32_t)rs[nr + 2 - kf]);
+  return cut;
+}
+
+// the final insertion sort of a <= 16-element part: a stable sort by score
+__device__ void WaveStableSort(unsigned long long *K, uint32_t first, uint32_t last, uint32_t lane) {
+  const uint32_t len = last - first;
+  unsigned long long v = 0;
+  uint32_t r = 0;
+  if (lane < len) {
+    v = K[first + lane];
+    const uint32_t sv = (uint32_t)(v >> 32);
+    for (uint32_t i = 0; i < len; ++i) {
+      const uint32_t si = (uint32_t)(K[first + i] >> 32);
+      r += (si > sv || (si == sv && i < lane)) ? 1u : 0u;
+    }
+  }
+  WaveSync();
+  if (lane < len) K[first + r] = v;
+  WaveSync();
+}
+
+__global__ __launch_bounds__(64 * kMergeWaves) void k_merge_wave(MergeArgs a) {
+  __shared__ unsigned long long s_key[kMergeWaves][kMergeCap];
+  __shared__ uint16_t s_ls[kMergeWaves][kMergeCap + 2];
+  __shared__ uint16_t s_rs[kMergeWaves][kMergeCap + 2];
+  __shared__ MergeFrame s_stack[kMergeWaves][64];
+  __shared__ uint32_t s_taken[kMergeWaves][kMergeBest];
+  const uint32_t lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t g = blockIdx.x * kMergeWaves + w;
+  if (g >= a.ng) return;
+  const uint32_t q0 = a.group_first[g], q1 = a.group_last[g];
+  const unsigned long long b = a.offsets[q0] - a.out_base;
+  const unsigned long long n64 = a.offsets[q1] + a.counts[q1] - a.out_base - b;
+  if (n64 > a.wave_cap) {
+    if (lane == 0) MergeGroup(a, g);
+    return;
+  }
+  const uint32_t n = (uint32_t)n64;
+  unsigned long long *K = s_key[w];
+  for (uint32_t i = lane; i < n; i += 64) K[i] = ((unsigned long long)a.score[b + i] << 32) | i;
+  MergeFrame *stk = s_stack[w];
+  uint32_t *taken = s_taken[w];
+  if (lane == 0 && n) stk[0] = MergeFrame{0u, n, 2 * stdsort::Lg((long)n)};
+  int sp = n ? 1 : 0;
+  WaveSync();
+  const ScoreDescending less;
+  const size_t so = (size_t)g * a.cap;
+  uint32_t count = 0, walked = 0, done = 0;
+  while (count < a.best && walked < n) {
+    if (walked == done) {
+      // LazySort::Advance on the wave: finalize the next partition
+      if (sp == 0) break;
+      MergeFrame f = stk[--sp];
+      bool heap = false;
+      while (f.last - f.first > (uint32_t)stdsort::kThreshold) {
+        if (f.depth == 0) {
+          if (lane == 0) stdsort::HeapSortRange(K + f.first, K + f.last, less);
+          WaveSync();
+          heap = true;
+          break;
+        }
+        --f.depth;
+        const uint32_t mid = f.first + (f.last - f.first) / 2;
+        if (lane == 0) stdsort::MoveMedianToFirst(K + f.first, K + f.first + 1, K + mid, K + f.last - 1, less);
+        WaveSync();
+        const uint32_t cut = WavePartition(K, f.first, f.last, s_ls[w], s_rs[w], lane);
+        if (lane == 0) stk[sp] = MergeFrame{cut, f.last, f.depth};
+        ++sp;
+        f.last = cut;
+      }
+      if (!heap) WaveStableSort(K, f.first, f.last, lane);
+      WaveSync();
+      done = f.last;
+    }
+    // the walk over finalized keys, up to 64 at a time, in order
+    const uint32_t m = min(64u, done - walked);
+    uint32_t sid = 0xFFFFFFFFu, c = 0;
+    bool ok = lane < m;
+    if (ok) {
+      c = (uint32_t)(b + (uint32_t)K[walked + lane]);
+      sid = SubjectOf(a.subj_start, a.nsubj, a.dblen, a.end[c]);
+      for (uint32_t k = 0; k < count; ++k) ok = ok && taken[k] != sid;
+    }
+    for (uint32_t t = 0; t + 1 < m; ++t) {
+      const uint32_t st = (uint32_t)__shfl((int)sid, (int)t);
+      if (lane > t && st == sid) ok = false;
+    }
+    const unsigned long long bal = __ballot(ok);
+    const uint32_t rank = __popcll(bal & ((1ull << lane) - 1));
+    const uint32_t take = min((uint32_t)__popcll(bal), a.best - count);
+    if (ok && rank < take) {
+      const uint32_t at = count + rank;
+      a.sel_sid[so + at] = sid;
+      a.sel_cand[so + at] = c;
+      a.tb_qid[so + at] = a.cand_qid[a.out_base + c];
+      a.tb_end[so + at] = a.end[c];
+      taken[at] = sid;
+    }
+    WaveSync();
+    count += take;
+    walked += m;
+  }
+  if (lane == 0) a.sel_count[g] = count;
+  for (uint32_t k = count + lane; k < a.cap; k += 64) a.tb_qid[so + k] = 0xFFFFFFFFu;
 }
 
 // One 20-byte record per selected hit, subject-relative like the reference's

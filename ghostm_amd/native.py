@@ -62,6 +62,8 @@ class GhostmStats(ctypes.Structure):
         ("score_rechecks", c_uint64),
         ("traceback_launches_scan", c_uint64),
         ("traceback_scan_cells", c_uint64),
+        ("merge_launches", c_uint64),
+        ("merge_launches_wave", c_uint64),
     ]
 
     def as_dict(self) -> dict:

@@ -144,6 +144,8 @@ typedef struct GhostmStats {
   uint64_t score_rechecks;        /* guarded f16 K2 candidates re-scored exactly in int16 */
   uint64_t traceback_launches_scan; /* K3 launches preceded by the scores-only scan (K3a) */
   uint64_t traceback_scan_cells;    /* K3a: sum over hits of L x reverse-window columns */
+  uint64_t merge_launches;          /* K4 launches */
+  uint64_t merge_launches_wave;     /* ... that ran one wave per name group (k_merge_wave) */
 } GhostmStats;
 
 /* Session: parse `aln` options exactly like the reference (getopt string

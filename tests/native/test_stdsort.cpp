@@ -14,17 +14,77 @@ struct Item {
   uint32_t score, idx;
 };
 
+// k_merge_wave's partition (ghostm_amd/csrc/kernels.h), restated sequentially
+// from the two stop lists of the input: left stops = positions in
+// [first+1, last) whose element is not less than the pivot (ascending), right
+// stops = positions in [first, last) the pivot is not less than (ascending,
+// used from the end). Pairs k = 1, 2, ... are swapped while the k-th left stop
+// lies below the k-th right stop from the end; the cut is the first failing
+// left stop, or the last swapped right stop when that comes first.
+template <class T, class Less> T *StopListPartition(T *first, T *last, Less less) {
+  std::vector<long> ls(1, 0), rs(1, 0);  // 1-based
+  for (T *x = first; x < last; ++x) {
+    if (x > first && !less(*x, *first)) ls.push_back(x - first);
+    if (!less(*first, *x)) rs.push_back(x - first);
+  }
+  const long nl = (long)ls.size() - 1, nr = (long)rs.size() - 1;
+  long kf = nl + 1;
+  for (long k = 1; k <= nl; ++k)
+    if (!(k <= nr && rs[nr + 1 - k] > ls[k])) { kf = k; break; }
+  for (long k = 1; k < kf; ++k) std::swap(first[ls[k]], first[rs[nr + 1 - k]]);
+  long cut = kf <= nl ? ls[kf] : (long)(last - first);
+  if (kf >= 2) cut = std::min(cut, rs[nr + 2 - kf]);
+  return first + cut;
+}
+
+// std::sort with that partition (otherwise stdsort::Sort's loop)
+template <class T, class Less> void StopListSort(T *first, long n, Less less) {
+  namespace ss = ghostm::stdsort;
+  if (n <= 0) return;
+  T *last = first + n;
+  struct Frame {
+    T *first, *last;
+    int depth;
+  };
+  std::vector<Frame> stack{Frame{first, last, ss::Lg(n) * 2}};
+  while (!stack.empty()) {
+    Frame f = stack.back();
+    stack.pop_back();
+    while (f.last - f.first > ss::kThreshold) {
+      if (f.depth == 0) {
+        ss::HeapSortRange(f.first, f.last, less);
+        break;
+      }
+      --f.depth;
+      T *mid = f.first + (f.last - f.first) / 2;
+      ss::MoveMedianToFirst(f.first, f.first + 1, mid, f.last - 1, less);
+      T *cut = StopListPartition(f.first, f.last, less);
+      stack.push_back(Frame{cut, f.last, f.depth});
+      f.last = cut;
+    }
+  }
+  if (n > ss::kThreshold) {
+    ss::InsertionSort(first, first + ss::kThreshold, less);
+    for (T *i = first + ss::kThreshold; i != last; ++i) ss::UnguardedLinearInsert(i, less);
+  } else {
+    ss::InsertionSort(first, last, less);
+  }
+}
+
 int main(int argc, char **argv) {
   const long trials = argc > 1 ? atol(argv[1]) : 200000;
   std::mt19937_64 rng(12345);
   auto less = [](const Item &a, const Item &b) { return a.score > b.score; };
   long bad = 0, total = 0;
-  long lazy_bad = 0;
+  long lazy_bad = 0, stop_bad = 0;
   auto check = [&](std::vector<Item> v) {
-    std::vector<Item> a = v, b = v, c = v;
+    std::vector<Item> a = v, b = v, c = v, d = v;
     std::sort(a.begin(), a.end(), less);
     ghostm::stdsort::Sort(b.data(), (long)b.size(), less);
+    StopListSort(d.data(), (long)d.size(), less);
     ++total;
+    for (size_t i = 0; i < a.size(); ++i)
+      if (a[i].idx != d[i].idx) { ++stop_bad; break; }
     for (size_t i = 0; i < a.size(); ++i)
       if (a[i].idx != b[i].idx) { ++bad; return; }
     // lazy form: every finalized prefix already equals std::sort's
@@ -71,7 +131,8 @@ int main(int argc, char **argv) {
     for (long i = 0; i < n; ++i)
       if (a[i].idx != b[i].idx) { ++heap_bad; break; }
   }
-  bad += heap_bad + lazy_bad;
+  bad += heap_bad + lazy_bad + stop_bad;
+  printf("stop-list partition (k_merge_wave): %ld mismatches\n", stop_bad);
   printf("lazy prefixes: %ld mismatches\n", lazy_bad);
   printf("heap fallback: %ld mismatches\n", heap_bad);
   printf("stdsort emulation: %ld arrays, %ld mismatches\n", total, bad);

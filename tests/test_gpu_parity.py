@@ -295,3 +295,25 @@ def test_traceback_scan_modes_match_golden(mode, ds, var, opts, dataset, golden,
         assert st["traceback_scan_cells"] > 0
         # the key DP runs only columns 0..j*: fewer cells than the scan covered
         assert st["traceback_cells"] < st["traceback_scan_cells"]
+
+
+@pytest.mark.parametrize("mode", ["thread", "wave", "wave_cap40"])
+@pytest.mark.parametrize("ds,var,opts", [("syn_small", "default", []), ("syn_small", "b3", ["-b", "3"]),
+                                         ("syn_small", "b20_t1", ["-b", "20", "-t", "1", "-y", "2"]),
+                                         ("syn_dna", "b5_y2", ["-b", "5", "-y", "2"]),
+                                         ("protein_testset", "y2", ["-y", "2"]),
+                                         ("syn_short", "default", [])])
+def test_merge_modes_match_golden(mode, ds, var, opts, dataset, golden, tmp_path):
+    """K4 with one thread per name group (k_merge) and with one wave per group
+    (k_merge_wave: wave-parallel partitions of std::sort's introsort in LDS);
+    wave_cap40 sends every group above 40 keys to the wave kernel's one-lane
+    fallback, so both branches run in one launch. Each reproduces the golden."""
+    d = dataset(ds)
+    env = {"GHOSTM_K4": "thread"} if mode == "thread" else {"GHOSTM_K4": "wave"}
+    if mode == "wave_cap40":
+        env["GHOSTM_K4_CAP"] = "40"
+    text, st = _gpu_text(d, opts, env, str(tmp_path / "g.out"))
+    (tmp_path / "g.out").write_bytes(text)
+    assert cases.sha256(str(tmp_path / "g.out")) == golden["aln"][f"{ds}/{var}"]["sha256"]
+    assert st["merge_launches"] > 0
+    assert st["merge_launches_wave"] == (0 if mode == "thread" else st["merge_launches"])
