@@ -122,7 +122,7 @@ struct DeviceModule::Impl {
 
 static constexpr uint32_t kSlotCap = 256;
 // K3a: the pair table (32 x 32 codes x 32 query codes, one word each) + histogram
-static constexpr size_t kScanLds = (size_t)kern::kPairCodes * 32 * 32 * 4 + kern::kSortBins * 4;
+static constexpr size_t kScanLds = (size_t)kern::kPairWords * 4 + kern::kSortBins * 4;
 
 DeviceModule &DeviceModule::Get() {
   static DeviceModule *m = new DeviceModule();

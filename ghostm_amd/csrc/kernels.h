@@ -1200,8 +1200,10 @@ __device__ inline int ShiftUpI(int v) { return __builtin_amdgcn_update_dpp(0, v,
 template <int S, int MLW, bool FINAL>
 __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
   using KL = KeyLayout<MLW>;
-  __shared__ int s_key[32 * 32];
-  for (uint32_t e = threadIdx.x; e < 32 * 32; e += kTbBlock) s_key[e] = a.mat_tb[e];
+  // rows of 33 dwords: lanes reading the same query code for different DB codes
+  // fall on different banks
+  __shared__ int s_key[32 * 33];
+  for (uint32_t e = threadIdx.x; e < 32 * 32; e += kTbBlock) s_key[(e >> 5) * 33 + (e & 31)] = a.mat_tb[e];
   __syncthreads();
 
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1256,7 +1258,7 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
       if (c == kSeqEnd) { done = true; active = false; }
     }
     if (active) {
-      const char *rowp = reinterpret_cast<const char *>(s_key) + c * 128;
+      const char *rowp = reinterpret_cast<const char *>(s_key) + MulU24(c, 33 * 4);
       auto T = [&](int u) { return *reinterpret_cast<const int *>(rowp + ((qoff[u >> 2] >> (8 * (u & 3))) & 0xFFu)); };
       int sd = kdiag0 + T(0), KF = kfin, kup = kin;
 #pragma unroll
@@ -1658,6 +1660,12 @@ __global__ void k_records(const uint32_t *sel_count, const SlotHit *slots, const
 constexpr uint32_t kSortBins = 1024;   // counting-sort keys (column counts), clamped
 constexpr int kScanBlock = 1024;       // one workgroup per CU: the pair table fills the LDS
 constexpr uint32_t kPairCodes = 26;    // DB codes 0..25 (25 = END) index the pair table
+// dwords per (a, b) code pair: query codes 0..31 plus one, an odd stride, so the
+// bank of entry (a, b, q), (pair * 33 + q) mod 32, spreads lanes reading the same
+// query code for different pairs over the banks (a stride of 32 put them all on
+// bank q: 20 amino-acid codes among a wave's 32 lanes of one ds_read_b32 group)
+constexpr uint32_t kPairStride = 33;
+constexpr uint32_t kPairWords = kPairCodes * kPairCodes * kPairStride;
 
 // Per slot: the reverse window (0 = empty slot; counted into *empty), ncols
 // reset to 0.
@@ -1832,15 +1840,17 @@ __global__ void k_rev_codes(const uint8_t *qseq, uint32_t nq, uint32_t L, uint32
 }
 
 // Pair table in LDS: word (a, b, q) = (M[a][q], M[b][q]) encoded in the two
-// halves; the byte offset ((a * 32 + b) << 7) + 4q is one SDWA add per row, and
-// one ds_read_b32 gives both hits' profile values, with no v_perm.
+// halves at dword (a * 26 + b) * kPairStride + q; the per-column pair base plus
+// the row's 4q is one SDWA add per row, and one ds_read_b32 gives both hits'
+// profile values, with no v_perm.
 template <int S, bool HALF, bool EXACT>
 __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
   using C = Cells<HALF>;
   extern __shared__ __attribute__((aligned(16))) uint32_t s_pair[];
-  uint32_t *s_hist = s_pair + kPairCodes * 32 * 32;
-  for (uint32_t e = threadIdx.x; e < kPairCodes * 32 * 32; e += kScanBlock) {
-    const uint32_t q = e & 31, cb = (e >> 5) & 31, ca = e >> 10;
+  uint32_t *s_hist = s_pair + kPairWords;
+  for (uint32_t e = threadIdx.x; e < kPairWords; e += kScanBlock) {
+    const uint32_t pr = e / kPairStride, q = e - pr * kPairStride;
+    const uint32_t ca = pr / kPairCodes, cb = pr - ca * kPairCodes;
     const int va = q == kPadCode ? kNeg16 : (ca < 25 && q < 25 ? a.mat[ca * 32 + q] : 0);
     const int vb = q == kPadCode ? kNeg16 : (cb < 25 && q < 25 ? a.mat[cb * 32 + q] : 0);
     s_pair[e] = (uint32_t)(unsigned short)C::Encode(va) | (uint32_t)(unsigned short)C::Encode(vb) << 16;
@@ -1942,7 +1952,8 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
         st = cell.At(end, prev_end);
         prev_end = end;
       }
-      const uint32_t cbase = (min(rA, kPairCodes - 1) << 12) | (rB << 7);
+      const uint32_t cbase = MadU24(min(rA, kPairCodes - 1), kPairCodes * kPairStride * 4,
+                                    MulU24(min(rB, kPairCodes - 1), kPairStride * 4));
       const char *tp = reinterpret_cast<const char *>(s_pair) + cbase;
       auto T = [&](int u) { return *reinterpret_cast<const uint32_t *>(tp + ((qoff[u >> 2] >> (8 * (u & 3))) & 0xFFu)); };
       uint32_t diag = diag0, F = fin, cm = 0;
