@@ -19,6 +19,7 @@
 #include <string>
 #include <vector>
 
+#include "../../include/ghostm_hip.h"
 #include "common.h"
 #include "formats.h"
 
@@ -77,14 +78,16 @@ int DbFormatMain(int argc, char **argv) {
   std::string in_path, out_prefix;
   uint32_t seed = (1u << 4) - 1;
   uint32_t max_concat = 1u << 27;
+  int device = -1;  // -D d (extension): build the k-mer index on GPU d
   optind = 1;
   int c;
-  while ((c = getopt(argc, argv, "i:o:k:l:")) >= 0) {
+  while ((c = getopt(argc, argv, "i:o:k:l:D:")) >= 0) {
     switch (c) {
       case 'i': in_path = optarg; break;
       case 'o': out_prefix = optarg; break;
       case 'k': seed = (1u << atoi(optarg)) - 1; break;
       case 'l': max_concat = atoi(optarg) * (1 << 20); break;
+      case 'D': device = atoi(optarg); break;
       default: throw std::invalid_argument("");
     }
   }
@@ -156,6 +159,19 @@ int DbFormatMain(int argc, char **argv) {
     {
       std::ofstream f((prefix + ".pos").c_str(), std::ios::binary);
       WriteRaw(f, starts.data(), starts.size());
+    }
+    if (device >= 0) {
+      std::vector<uint32_t> kc(kcl), pos(len);
+      uint32_t npos = 0;
+      if (GhostmBuildIndexGpu(data.data(), len, seed, kcl, kc.data(), pos.data(), &npos, device, nullptr))
+        throw Error(std::string("db -D: ") + GhostmGetLastError());
+      std::ofstream f((prefix + ".ind").c_str(), std::ios::binary);
+      WriteRaw(f, &seed, 1);
+      WriteRaw(f, &kcl, 1);
+      WriteRaw(f, &npos, 1);
+      WriteRaw(f, kc.data(), kc.size());
+      WriteRaw(f, pos.data(), npos);
+      continue;
     }
     // counting-sort k-mer index; windows containing X (anywhere in the seed span)
     // are skipped, subjects not longer than the seed span contribute nothing

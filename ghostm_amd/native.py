@@ -86,6 +86,8 @@ SIGNATURES = {
     "GhostmBuildInfo": (c_char_p, []),
     "CountCandidatesGpu": (c_int, [c_uint32] * 6 + [u32p]),
     "TraceBackGpu": (c_int, [c_uint32, u32p, u32p, c_uint32, c_uint32, c_int, c_int, u32p, u32p, u32p, POINTER(c_float)]),
+    "GhostmBuildIndexGpu": (c_int, [POINTER(ctypes.c_uint8), c_uint32, c_uint32, c_uint32, u32p, u32p, u32p, c_int,
+                                    POINTER(c_float)]),
     "GhostmSessionCreate": (c_void_p, [c_int, POINTER(c_char_p)]),
     "GhostmSessionRun": (c_int, [c_void_p]),
     "GhostmSessionOutput": (c_size_t, [c_void_p, c_char_p, c_size_t]),

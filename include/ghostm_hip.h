@@ -105,6 +105,17 @@ int TraceBackGpu(uint32_t nhits, const uint32_t query_ids[], const uint32_t db_e
                  int open_gap, int extend_gap, uint32_t db_starts[], uint32_t aln_lens[],
                  uint32_t aln_matches[], float seq_ids[]);
 
+/* The `db` formatter's k-mer index of one DB chunk, built on the GPU
+ * (replaces DBCreator::ConstructIndex, db_creator.cpp:167-241).
+ * seq[len] = the chunk's END-separated residues (.seq); seed = the index seed mask
+ * (db -k k -> 2^k - 1); kcl = 32^weight(seed) + 1. Fills keys_count[kcl] (CSR
+ * offsets) and positions[*npos] (ascending per key; the array must hold len
+ * entries) byte-identical to the CPU formatter's .ind. device_ms (optional)
+ * receives the device time of the build (HIP events, after the upload). */
+int GhostmBuildIndexGpu(const uint8_t *seq, uint32_t len, uint32_t seed, uint32_t kcl,
+                        uint32_t *keys_count, uint32_t *positions, uint32_t *npos, int device,
+                        float *device_ms);
+
 /* One resolved hit, the record gathered across ranks (32 bytes). Coordinates are
  * subject-relative, as printed minus one. */
 typedef struct GhostmHit {
