@@ -710,6 +710,7 @@ void Session::Run() {
   stats_.traceback_scan_cells = dt.traceback_scan_cells;
   stats_.merge_launches = dt.merge_launches;
   stats_.merge_launches_wave = dt.merge_launches_wave;
+  stats_.score_launches_framed = dt.score_launches_framed;
   for (size_t k = 0; k < used_parts_; ++k)
     for (const auto &h : parts_[k].hits) stats_.hits += h.size();
 }

@@ -53,6 +53,7 @@ struct DeviceTimes {
   uint64_t seed_launches_hash = 0;  // Seed() calls whose slot pass used k_seed_hash
   uint64_t score_rechecks = 0;      // guarded f16 candidates re-scored in int16
   uint64_t traceback_launches_scan = 0, traceback_scan_cells = 0;  // K3a scores-only pass
+  uint64_t score_launches_framed = 0;  // f16 K2 launches of the column-framed kernel (k_score16f)
   uint64_t merge_launches = 0, merge_launches_wave = 0;            // K4 (k_merge_wave: one wave per group)
 };
 

@@ -529,7 +529,11 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
   // f16 is exact below 2048; beyond that it runs with a guard and the int16
   // kernel re-scores the (rare) candidates whose best reaches it
   const bool half = packed && !(force && strcmp(force, "int16") == 0);
-  int guard = bound < 2048 ? 0 : 2000;
+  // the column-framed f16 kernel (k_score16f) holds values up to best + the
+  // largest frame, (steps + 1) * ext_pen; GHOSTM_K2=f16plain keeps k_score16<S, true>
+  const int64_t sigma_max = (int64_t)(base + lay.G) * (-gap.ext);
+  const bool framed = half && sigma_max <= 1000 && !(force && strcmp(force, "f16plain") == 0);
+  int guard = framed ? (bound + sigma_max < 2048 ? 0 : (int)(2040 - sigma_max)) : (bound < 2048 ? 0 : 2000);
   if (half && getenv("GHOSTM_K2_GUARD")) guard = atoi(getenv("GHOSTM_K2_GUARD"));  // tests: force re-scores
   const uint32_t per_block = (kern::kScoreBlock / 64) * lay.gpw * (packed ? 2 : 1);
   // tasks: runs of <= per_block consecutive candidates spanning <= Qmax queries
@@ -602,15 +606,18 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
   if (packed) {
     switch (lay.S) {
       case 32:
-        if (half) hipLaunchKernelGGL((kern::k_score16<32, true>), grid, block, lds, S(stream_), a);
+        if (framed) hipLaunchKernelGGL((kern::k_score16f<32>), grid, block, lds, S(stream_), a);
+        else if (half) hipLaunchKernelGGL((kern::k_score16<32, true>), grid, block, lds, S(stream_), a);
         else hipLaunchKernelGGL((kern::k_score16<32, false>), grid, block, lds, S(stream_), a);
         break;
       case 16:
-        if (half) hipLaunchKernelGGL((kern::k_score16<16, true>), grid, block, lds, S(stream_), a);
+        if (framed) hipLaunchKernelGGL((kern::k_score16f<16>), grid, block, lds, S(stream_), a);
+        else if (half) hipLaunchKernelGGL((kern::k_score16<16, true>), grid, block, lds, S(stream_), a);
         else hipLaunchKernelGGL((kern::k_score16<16, false>), grid, block, lds, S(stream_), a);
         break;
       default:
-        if (half) hipLaunchKernelGGL((kern::k_score16<8, true>), grid, block, lds, S(stream_), a);
+        if (framed) hipLaunchKernelGGL((kern::k_score16f<8>), grid, block, lds, S(stream_), a);
+        else if (half) hipLaunchKernelGGL((kern::k_score16<8, true>), grid, block, lds, S(stream_), a);
         else hipLaunchKernelGGL((kern::k_score16<8, false>), grid, block, lds, S(stream_), a);
         break;
     }
@@ -659,6 +666,7 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
   times_.score_launches += 1;
   times_.score_launches_packed += packed ? 1 : 0;
   times_.score_launches_half += half ? 1 : 0;
+  times_.score_launches_framed += framed ? 1 : 0;
   times_.score_cells += cells;
 }
 

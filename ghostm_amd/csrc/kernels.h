@@ -1026,6 +1026,204 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16(ScoreArgs a) {
                                              : 0ull);
 }
 
+// k_score16f<S>: the f16 kernel with the E chain's decay absorbed by a column
+// frame. Column j holds every value as X + sigma_j per half, sigma_j = (columns
+// since the last END or the window start) * ext_pen, so with ext <= 0:
+//   s^ = H^(diag) + (M + ext_pen)                  (profile carries the step)
+//   h^ = max3(s^, E^, F^)
+//   oE = h^ + (open - ext)
+//   E^ = max3(E^, oE, sigma_{j+1})                 E(j+1) = max(E + ext, h + open, 0)
+//   F^ = max(F^, oE) + ext                          F(k+1) = max(F + ext, h + open)
+// 6 packed ops per row pair instead of 7 (F is left unclamped: with E >= 0,
+// max(s, E, F) is the same whether F is floored at 0 or not, since ext <= 0).
+// The column max is framed uniformly, so the real one is cm^ - sigma_j.
+// END columns: the diagonal into the next column is masked as in k_score16
+// (fma with m = 0) and the frame restarts there (sigma = ext_pen, real 0 = p);
+// E cannot be reset through its penalty any more, so a branch taken only on
+// steps where some lane meets END writes E^ = sigma_{j+1} into those halves.
+// Values are exact while every framed value stays below 2048: best + the
+// largest frame (steps * ext_pen); beyond that the guard re-scores in int16.
+template <int S>
+__global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
+  using C = Cells<true>;
+  extern __shared__ __attribute__((aligned(16))) short s_prof16[];
+  const ScoreTask t = a.tasks[blockIdx.x];
+  const uint32_t RS = a.Lpad + 8;
+  const int extp = -a.ext;
+
+  const uint32_t per_slot = kProfRows16 * a.Lpad;
+  const uint32_t total = t.q_count * per_slot;
+  for (uint32_t e = threadIdx.x; e < total; e += kScoreBlock) {
+    const uint32_t slot = e / per_slot, rem = e - slot * per_slot;
+    const uint32_t c = rem / a.Lpad, r = rem - c * a.Lpad;
+    int v = kNeg16;
+    if (r >= a.pad) v = (c < 25 ? a.mat[c * 32 + a.qseq[(size_t)(t.q_first + slot) * a.L + (r - a.pad)]] : 0) + extp;
+    s_prof16[(slot * kProfRows16 + c) * RS + r] = C::Encode(v);
+  }
+  __syncthreads();
+
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t g = lane / a.G, i = lane - g * a.G;
+  const uint32_t pair = wave * a.gpw + g;
+  const bool in_group = g < a.gpw;
+  const bool vA = in_group && 2 * pair < t.count;
+  const bool vB = in_group && 2 * pair + 1 < t.count;
+  const unsigned long long cA = t.begin + 2 * pair, cB = cA + 1;
+  uint32_t slotA = 0, slotB = 0, offA = 0, offB = 0, wA = 0, wB = 0;
+  if (vA) {
+    slotA = a.cand_qid[cA] - t.q_first;
+    int o = (int)(a.cand_start[cA] - a.extend);
+    offA = o < 0 ? 0u : (uint32_t)o;
+    wA = a.base;
+    if (offA + wA > a.dblen) wA = a.dblen - offA;
+  }
+  if (vB) {
+    slotB = a.cand_qid[cB] - t.q_first;
+    int o = (int)(a.cand_start[cB] - a.extend);
+    offB = o < 0 ? 0u : (uint32_t)o;
+    wB = a.base;
+    if (offB + wB > a.dblen) wB = a.dblen - offB;
+  }
+  const uint32_t baseA2 = (slotA * kProfRows16 * RS + i * S) * 2;
+  const uint32_t baseB2 = (slotB * kProfRows16 * RS + i * S) * 2;
+  const uint8_t *dbp = a.db - kDbFrontPad;
+  const uint32_t back = kDbFrontPad + a.dblen;
+  const uint32_t xA = (vA ? offA + kDbFrontPad : back) - i, xB = (vB ? offB + kDbFrontPad : back) - i;
+  const uint32_t RS2 = RS * 2;
+  const uint32_t EXTP = C::Pair(extp);
+  const hf2 KOE = HF(C::Pair(a.open - a.ext));
+  const hf2 NEXT = HF(C::Pair(a.ext));
+
+  uint32_t H[S], E[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) { H[k] = 0; E[k] = EXTP; }
+  uint32_t sig = EXTP;                   // frame of the current column (real 0), per half
+  uint32_t best = 0, col = 0;
+  uint32_t jj = ((0u - i) & 0xFFFFu) * 0x10001u;
+  uint32_t nend = 0;
+  uint32_t hout = 0, fout = 0, hprev = 0;
+  uint32_t prev_end = 0xFFFFFFFFu;
+  uint32_t c0A = dbp[xA], c0B = dbp[xB], c1A = dbp[xA + 1], c1B = dbp[xB + 1];
+  const uint32_t steps = a.base + a.G - 1;
+  const uint32_t wA_ = vA ? wA : 0u, wB_ = vB ? wB : 0u;
+  auto column = [&](uint32_t step, auto tested_c) {
+    constexpr bool tested = decltype(tested_c)::value;
+    uint32_t hin = ShiftUp(hout), fin = ShiftUp(fout);
+    if (i == 0) { hin = sig; fin = 0; }  // real 0 for H; any real F <= 0 will do
+    const uint32_t diag0 = hprev;
+    hprev = hin;
+    uint32_t rA = c0A, rB = c0B;
+    if constexpr (tested) {
+      const uint32_t j = step - i;
+      rA = j < wA_ ? rA : kSeqEnd;
+      rB = j < wB_ ? rB : kSeqEnd;
+    }
+    c0A = c1A;
+    c0B = c1B;
+    const uint8_t *colp = dbp + step + 2;
+    c1A = colp[xA];
+    c1B = colp[xB];
+    const uint32_t rr = rA | (rB << 16);
+    const uint32_t end = PkSign(PkAddU16(rr, 0x7FE77FE7u));
+    const hf2 m = HF(C::kOne & ~prev_end);
+    prev_end = end;
+    // the next column's frame: one step on, or restarted after END
+    const uint32_t zn = BfiV(end, EXTP, W(HF(sig) + HF(EXTP)));
+    const hf2 Z1 = HF(zn);
+    const char *pA = reinterpret_cast<const char *>(s_prof16) + MadU24(rA, RS2, baseA2);
+    const char *pB = reinterpret_cast<const char *>(s_prof16) + MadU24(rB, RS2, baseB2);
+    uint32_t diag = diag0, F = fin, cm = 0;
+#pragma unroll
+    for (int k = 0; k < S; k += 8) {
+      const uint4 qa = *reinterpret_cast<const uint4 *>(pA + 2 * k);
+      const uint4 qb = *reinterpret_cast<const uint4 *>(pB + 2 * k);
+      const uint32_t wa[4] = {qa.x, qa.y, qa.z, qa.w}, wb[4] = {qb.x, qb.y, qb.z, qb.w};
+      // row u's profile pair (perm) and diagonal sum, formed from the previous
+      // column's H[k + u - 1] before row u - 1 overwrites it
+      auto prof = [&](int u) {
+        return __builtin_amdgcn_perm(wb[u >> 1], wa[u >> 1], (u & 1) ? 0x07060302u : 0x05040100u);
+      };
+      uint32_t s[8];
+      s[0] = C::Diag(diag, m, prof(0));
+      s[1] = C::Diag(H[k], m, prof(1));
+      diag = H[k + 7];
+      // row u + 2's perm and diagonal sum and row u's E update sit between the
+      // dependent steps h -> oE -> max -> F, so few packed ops read the result
+      // of the instruction right before them (VOP3P forwarding nops)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const hf2 h = __builtin_elementwise_maximum(__builtin_elementwise_maximum(HF(s[u]), HF(E[k + u])), HF(F));
+        uint32_t p2 = 0;
+        if (u + 2 < 8) p2 = prof(u + 2);
+        H[k + u] = W(h);
+        const hf2 oE = h + KOE;
+        if (u + 2 < 8) s[u + 2] = C::Diag(H[k + u + 1], m, p2);
+        const hf2 G = __builtin_elementwise_maximum(HF(F), oE);
+        E[k + u] = W(__builtin_elementwise_maximum(__builtin_elementwise_maximum(HF(E[k + u]), oE), Z1));
+        F = W(G + NEXT);
+      }
+      cm = C::Max3(C::Max3(H[k], H[k + 1], H[k + 2]), C::Max3(H[k + 3], H[k + 4], H[k + 5]),
+                   C::Max3(H[k + 6], H[k + 7], cm));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    hout = H[S - 1];
+    fout = F;
+    // END halves: E restarts at real 0 in the new frame (H needs nothing: the
+    // next column masks the diagonal, and F restarts from the lane above)
+    if (__builtin_amdgcn_ballot_w64(end != 0)) {  // wave-uniform: a real branch
+#pragma unroll
+      for (int k = 0; k < S; ++k) E[k] = BfiV(end, zn, E[k]);
+    }
+    const uint32_t cmr = W(HF(cm) - HF(sig));  // real column maximum (>= 0 off END)
+    const uint32_t keep = PkSign(PkSubI16(cmr, best)) | end;
+    best = BfiV(keep, best, cmr);
+    col = BfiV(keep, col, jj);
+    jj = PkAddU16(jj, 0x00010001u);
+    nend = PkAddU16(nend, end);
+    sig = zn;
+  };
+  const uint32_t fill = min(a.G - 1, steps);
+  uint32_t step = 0;
+  for (; step < fill; ++step) column(step, std::true_type{});
+  for (; step < a.base; ++step) column(step, std::false_type{});
+  for (; step < steps; ++step) column(step, std::true_type{});
+  const uint32_t ncolsA = steps - ((0x10000u - (nend & 0xFFFFu)) & 0xFFFFu);
+  const uint32_t ncolsB = steps - ((0x10000u - (nend >> 16)) & 0xFFFFu);
+  int BA = C::Decode(best & 0xFFFFu), CA = (int)(col & 0xFFFFu);
+  int BB = C::Decode(best >> 16), CB = (int)(col >> 16);
+  for (uint32_t k = 1; k < a.G; ++k) {
+    const int src = (int)(g * a.G + k);
+    const int oba = __shfl(BA, src), oca = __shfl(CA, src);
+    const int obb = __shfl(BB, src), ocb = __shfl(CB, src);
+    if (oba > BA || (oba == BA && oca > CA)) { BA = oba; CA = oca; }
+    if (obb > BB || (obb == BB && ocb > CB)) { BB = obb; CB = ocb; }
+  }
+  if (i == 0) {
+    if (vA) {
+      a.score_out[cA - a.out_base] = (uint32_t)BA;
+      a.end_out[cA - a.out_base] = offA + (uint32_t)CA;
+    }
+    if (vB) {
+      a.score_out[cB - a.out_base] = (uint32_t)BB;
+      a.end_out[cB - a.out_base] = offB + (uint32_t)CB;
+    }
+    if (a.guard) {
+      if (vA && BA >= a.guard) {
+        const uint32_t k = atomicAdd(a.guard_count, 1u);
+        a.guard_list[2 * k] = (uint32_t)(cA - a.out_base);
+        a.guard_list[2 * k + 1] = t.q_first + slotA;
+      }
+      if (vB && BB >= a.guard) {
+        const uint32_t k = atomicAdd(a.guard_count, 1u);
+        a.guard_list[2 * k] = (uint32_t)(cB - a.out_base);
+        a.guard_list[2 * k + 1] = t.q_first + slotB;
+      }
+    }
+  }
+  WaveAddCells(a.cells, (in_group && i == 0) ? (unsigned long long)((vA ? ncolsA : 0u) + (vB ? ncolsB : 0u)) * a.L
+                                             : 0ull);
+}
+
 // ------------------------------------------------------------------ K3 traceback
 constexpr int kTbBlock = 256;
 

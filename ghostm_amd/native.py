@@ -64,6 +64,7 @@ class GhostmStats(ctypes.Structure):
         ("traceback_scan_cells", c_uint64),
         ("merge_launches", c_uint64),
         ("merge_launches_wave", c_uint64),
+        ("score_launches_framed", c_uint64),
     ]
 
     def as_dict(self) -> dict:

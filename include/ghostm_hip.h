@@ -157,6 +157,7 @@ typedef struct GhostmStats {
   uint64_t traceback_scan_cells;    /* K3a: sum over hits of L x reverse-window columns */
   uint64_t merge_launches;          /* K4 launches */
   uint64_t merge_launches_wave;     /* ... that ran one wave per name group (k_merge_wave) */
+  uint64_t score_launches_framed;   /* f16 K2 launches of the column-framed kernel (k_score16f) */
 } GhostmStats;
 
 /* Session: parse `aln` options exactly like the reference (getopt string
