@@ -214,7 +214,11 @@ def main() -> None:
         packed = per["score_launches_packed"] == per["score_launches"] and per["score_launches"] > 0
         half = packed and per["score_launches_half"] == per["score_launches"]
         peak = PEAK_VALU_PK16_TOPS if packed else PEAK_VALU_TOPS
-        if half:
+        framed = half and per.get("score_launches_framed", 0) == per["score_launches"]
+        if framed:
+            kname = ("k_score16f<32> (K2 Gotoh DP, packed f16 holding exact integers in a per-column frame, "
+                     "two candidates per lane)")
+        elif half:
             kname = "k_score16<32,f16> (K2 Gotoh DP, packed f16 holding exact integers, two candidates per lane)"
         elif packed:
             kname = "k_score16<32,int16> (K2 Gotoh DP, packed int16, two candidates per lane)"
@@ -265,12 +269,13 @@ def main() -> None:
             },
             "roofline_hbm": {
                 "bound": "hbm",
-                "kernel": "k_seed (K1 seed lookup, gathers of CSR positions)",
+                "kernel": "K1 seed stage per step (k_seed_lists, k_seed_hash, k_compact: gathers of CSR positions)",
                 "achieved": seed_gbs,
                 "peak": PEAK_HBM_GBS,
                 "unit": "GB/s",
                 "frac": seed_gbs / PEAK_HBM_GBS,
-                "traffic": pmc.get("k_seed_hbm_bytes_per_launch") if (pmc and pmc.get("queries") == args.queries) else None,
+                "algorithmic_bytes_per_step": per["seed_bytes"],
+                "traffic": pmc.get("k1_hbm_bytes_per_step") if (pmc and pmc.get("queries") == args.queries) else None,
             },
             "stages_s_per_step": {
                 "total": per["seconds_total"],

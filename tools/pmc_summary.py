@@ -58,6 +58,7 @@ def main() -> None:
     ap.add_argument("--round", required=True)
     ap.add_argument("--prof", required=True)
     ap.add_argument("--queries", type=int, required=True)
+    ap.add_argument("--trace-runs", type=int, default=3, help="session runs in the traced command (warmup + steps)")
     args = ap.parse_args()
     prof = os.path.join(REPO, "profiles")
     os.makedirs(prof, exist_ok=True)
@@ -108,10 +109,15 @@ def main() -> None:
         k = max(best, key=lambda x: kernels[x].get("percent_of_gpu_time", 0))
         return kernels[k]["hbm_bytes_per_launch"]
 
+    # K1 = every seed-stage kernel; per bench step = bytes per launch x launches
+    # in the trace / runs in the trace (warmup + steps of the traced command)
+    k1 = [k for k in kernels if k.startswith(("k_seed", "k_compact")) and "hbm_bytes_per_launch" in kernels[k]]
+    k1_step = sum(kernels[k]["hbm_bytes_per_launch"] * kernels[k].get("launches_in_trace", 0) for k in k1)
     traffic = {"round": args.round, "queries": args.queries,
                "note": "HBM bytes per launch = FETCH_SIZE*2*1024 + WRITE_SIZE*1024 (gfx950 correction)",
                "k_score_hbm_bytes_per_launch": fam("k_score"),
-               "k_seed_hbm_bytes_per_launch": fam("k_seed<")}
+               "k1_hbm_bytes_per_step": k1_step / args.trace_runs if k1 else None,
+               "k1_kernels": sorted(k1)}
     with open(os.path.join(prof, "pmc_traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1)
     print(json.dumps(traffic))
