@@ -379,18 +379,30 @@ void Session::DeviceMergePath(QueryData &q, DbData &d, const std::vector<uint32_
   const uint64_t kSegmentCands = 8ull << 20, kTailCands = 1ull << 20;
   const uint32_t ng = (uint32_t)q.group_first.size();
   auto group_begin = [&](uint32_t g) { return offsets[q.group_first[g]]; };
-  uint32_t g0 = 0;
-  while (g0 < ng) {
+  // segment cuts (group ranges) first, so each segment's K2 tasks can be built
+  // on the host while the previous segment's K2 runs
+  std::vector<std::pair<uint32_t, uint32_t>> cuts;
+  for (uint32_t g0 = 0; g0 < ng;) {
     const uint64_t rem = total - group_begin(g0);
     const uint64_t target =
         (rem > kTailCands && rem <= kSegmentCands + kTailCands) ? rem - kTailCands : kSegmentCands;
     uint32_t g1 = g0 + 1;
     while (g1 < ng && group_begin(g1) - group_begin(g0) < target) ++g1;
-    const uint64_t c0 = group_begin(g0);
-    const uint64_t c1 = g1 < ng ? group_begin(g1) : total;
+    cuts.emplace_back(g0, g1);
+    g0 = g1;
+  }
+  std::vector<DeviceModule::ScoreSegment> segs;
+  for (const auto &c : cuts) {
+    const uint64_t c0 = group_begin(c.first), c1 = c.second < ng ? group_begin(c.second) : total;
+    segs.push_back({c0, c1 - c0, q.group_first[c.first], q.group_last[c.second - 1] + 1});
+  }
+  for (size_t k = 0; k < cuts.size(); ++k) {
+    const uint32_t g0 = cuts[k].first, g1 = cuts[k].second;
+    const uint64_t c0 = segs[k].cand_begin, c1 = c0 + segs[k].n;
     if (c1 > c0) {
-      dev.Score(q.dev, d.dev, c0, c1 - c0, q.group_first[g0], q.group_last[g1 - 1] + 1, counts, offsets,
-                base, gap, nullptr, nullptr);
+      // the next segment's K2 tasks are built while this one's K2 runs
+      dev.Score(q.dev, d.dev, c0, c1 - c0, segs[k].q_first, segs[k].q_end, counts, offsets, base, gap, nullptr,
+                nullptr, k + 1 < segs.size() ? &segs[k + 1] : nullptr);
     }
     auto sel_counts = std::make_shared<std::vector<uint32_t>>();
     auto sel_hits = std::make_shared<std::vector<SelectedHit>>();
@@ -411,7 +423,6 @@ void Session::DeviceMergePath(QueryData &q, DbData &d, const std::vector<uint32_
       FormatSelected(*qp, g0, *sel_counts, *sel_hits, cap, part);
       stats_.seconds_output += NowSeconds() - t;
     });
-    g0 = g1;
   }
   stats_.batches += 1;
 }

@@ -59,6 +59,7 @@ struct DeviceTimes {
 
 class DeviceModule {
  public:
+  struct Impl;  // device.hip
   static DeviceModule &Get();
 
   void Bind(int device);                 // hipSetDevice + stream; idempotent
@@ -87,11 +88,19 @@ class DeviceModule {
 
   // K2 over candidates [cand_begin, cand_begin + n) whose queries are
   // [q_first, q_end) with per-query counts/offsets as returned by Seed.
-  // Scores/ends land in host arrays score[n], end[n].
+  // Scores/ends land in host arrays score[n], end[n] (when not null). With
+  // `next`, the host builds and uploads the next segment's tasks while this
+  // launch runs, and the Score() call for that segment launches at once.
+  struct ScoreSegment {
+    uint64_t cand_begin, n;
+    uint32_t q_first, q_end;
+  };
   void Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n, uint32_t q_first,
              uint32_t q_end, const std::vector<uint32_t> &counts,
              const std::vector<uint64_t> &offsets, uint32_t base_search_length,
-             const GapConfig &gap, uint32_t *score, uint32_t *end);
+             const GapConfig &gap, uint32_t *score, uint32_t *end, const ScoreSegment *next = nullptr);
+
+  uint32_t ScorePerBlock(DevQuery *q, uint32_t base_search_length, const GapConfig &gap) const;
 
   // K4 + K3 for a batch that covers every group of the chunk and starts from
   // empty result lists (first batch, first DB chunk): the reference Merge
@@ -117,19 +126,27 @@ class DeviceModule {
                  uint32_t base_search_length, int open, int ext, uint32_t *db_start,
                  uint32_t *aln_len, uint32_t *aln_match, float *seq_id);
 
-  DeviceTimes &times() { return times_; }
-  void ResetTimes() { times_ = DeviceTimes(); }
+  // resolves the launch timings and counters left pending by the no-wait paths
+  DeviceTimes &times() {
+    FlushTimes();
+    return times_;
+  }
+  void ResetTimes() {
+    FlushTimes();
+    times_ = DeviceTimes();
+  }
+  void FlushTimes();
   void Synchronize();
 
  private:
   DeviceModule() = default;
+  void UploadNextTasks(const ScoreSegment *next, uint32_t per_block);
   // span: runs of slots whose hits may pair (a name group's slots)
   void LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, const DevDb *d, uint32_t span);
   int device_ = -1;
   void *stream_ = nullptr;
   DeviceTimes times_;
   uint64_t records_ = 0;
-  struct Impl;
   Impl *impl_ = nullptr;
   friend struct DeviceModuleAccess;
 };

@@ -117,6 +117,24 @@ struct DeviceModule::Impl {
   DevBuf keys, sel_count, sel_cand, sel_sid, slot_hits;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   DevBuf counters;  // u64 [0] score cells, [1] traceback cells, [2] K3a scan cells
+  // K2 tasks of the next segment, built while the current one runs
+  struct Prepared {
+    uint64_t cand_begin, n, off;
+    uint32_t count, per_block;
+  };
+  DevBuf tasks_all;
+  std::vector<Prepared> prepared;
+  std::vector<kern::ScoreTask> next_tasks;  // host copy, alive until the next upload
+  // launch timings resolved after the run (no host wait per launch)
+  struct Pending {
+    hipEvent_t a, b;
+    double *dst;
+  };
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+  std::vector<Pending> pending;
+  DevBuf acc;        // u64 [0]: K2 cells of deferred launches
+  bool acc_zeroed = false;
   bool matrix_set = false;
 };
 
@@ -508,41 +526,15 @@ void DeviceModule::CopyStarts(uint64_t begin, uint64_t n, uint32_t *out) {
   HIP_CHECK(hipMemcpy(out, impl_->cand_start.as<uint32_t>() + begin, n * 4, hipMemcpyDeviceToHost));
 }
 
-void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n, uint32_t q_first,
-                         uint32_t q_end, const std::vector<uint32_t> &counts,
-                         const std::vector<uint64_t> &offsets, uint32_t base,
-                         const GapConfig &gap, uint32_t *score, uint32_t *end) {
-  Impl &I = *impl_;
-  if (n == 0) return;
-  if (gap.ext > 0) throw Error("positive gap extension score is not supported");
-  const Layout lay = ChooseLayout(q->L, base);
-  // packed int16 path (two candidates per lane) whenever every value fits
-  int max_abs = 0;
-  for (int v : I.h_matrix) max_abs = std::max(max_abs, v < 0 ? -v : v);
-  // encoding: f16 pairs when every score fits the exact-integer range of f16,
-  // else int16 pairs, else int32 (GHOSTM_K2=int32|int16|f16 restricts the choice)
-  const char *force = getenv("GHOSTM_K2");
-  const bool gaps_ok = gap.open <= 0 && gap.ext <= 0 && -gap.open < 2000 && -gap.ext < 2000;
-  const int64_t bound = (int64_t)q->L * max_abs;
-  const bool allow_packed = !(force && strcmp(force, "int32") == 0);
-  const bool packed = allow_packed && gaps_ok && bound < 30000 && base + 64 < kDbBack;
-  // f16 is exact below 2048; beyond that it runs with a guard and the int16
-  // kernel re-scores the (rare) candidates whose best reaches it
-  const bool half = packed && !(force && strcmp(force, "int16") == 0);
-  // the column-framed f16 kernel (k_score16f) holds values up to best + the
-  // largest frame, (steps + 1) * ext_pen; GHOSTM_K2=f16plain keeps k_score16<S, true>
-  const int64_t sigma_max = (int64_t)(base + lay.G) * (-gap.ext);
-  const bool framed = half && sigma_max <= 1000 && !(force && strcmp(force, "f16plain") == 0);
-  int guard = framed ? (bound + sigma_max < 2048 ? 0 : (int)(2040 - sigma_max)) : (bound < 2048 ? 0 : 2000);
-  if (half && getenv("GHOSTM_K2_GUARD")) guard = atoi(getenv("GHOSTM_K2_GUARD"));  // tests: force re-scores
-  const uint32_t per_block = (kern::kScoreBlock / 64) * lay.gpw * (packed ? 2 : 1);
-  // tasks: runs of <= per_block consecutive candidates spanning <= Qmax queries
-  std::vector<kern::ScoreTask> tasks;
-  tasks.reserve(n / per_block + (q_end - q_first) / kern::kScoreQmax + 2);
+// K2 tasks: runs of <= per_block consecutive candidates spanning <= Qmax queries
+static void BuildScoreTasks(uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32_t q_end,
+                            const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets,
+                            uint32_t per_block, std::vector<kern::ScoreTask> *tasks) {
+  tasks->reserve(tasks->size() + n / per_block + (q_end - q_first) / kern::kScoreQmax + 2);
   kern::ScoreTask cur{};
   bool open_task = false;
   auto flush = [&]() {
-    if (open_task && cur.count) tasks.push_back(cur);
+    if (open_task && cur.count) tasks->push_back(cur);
     open_task = false;
   };
   const uint64_t cand_end = cand_begin + n;
@@ -564,11 +556,105 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
     }
   }
   flush();
-  I.tasks.Reserve(tasks.size() * sizeof(kern::ScoreTask));
+}
+
+// the packed K2 encodings (two candidates per lane) whenever every value fits
+static bool ScorePacked(const int *h_matrix, uint32_t L, uint32_t base, const GapConfig &gap) {
+  int max_abs = 0;
+  for (int k = 0; k < 32 * 32; ++k) max_abs = std::max(max_abs, h_matrix[k] < 0 ? -h_matrix[k] : h_matrix[k]);
+  const char *force = getenv("GHOSTM_K2");
+  const bool gaps_ok = gap.open <= 0 && gap.ext <= 0 && -gap.open < 2000 && -gap.ext < 2000;
+  const int64_t bound = (int64_t)L * max_abs;
+  const bool allow_packed = !(force && strcmp(force, "int32") == 0);
+  return allow_packed && gaps_ok && bound < 30000 && base + 64 < kDbBack;
+}
+
+uint32_t DeviceModule::ScorePerBlock(DevQuery *q, uint32_t base, const GapConfig &gap) const {
+  const Layout lay = ChooseLayout(q->L, base);
+  return (kern::kScoreBlock / 64) * lay.gpw * (ScorePacked(impl_->h_matrix, q->L, base, gap) ? 2 : 1);
+}
+
+static unsigned long long *AccCells(DeviceModule::Impl &I, hipStream_t st) {
+  I.acc.Reserve(16);
+  if (!I.acc_zeroed) {
+    HIP_CHECK(hipMemsetAsync(I.acc.p, 0, 16, st));
+    I.acc_zeroed = true;
+  }
+  return I.acc.as<unsigned long long>();
+}
+
+static void NewEventPair(DeviceModule::Impl &I, hipEvent_t *a, hipEvent_t *b) {
+  while (I.ev_pool.size() < I.ev_used + 2) {
+    hipEvent_t e;
+    HIP_CHECK(hipEventCreate(&e));
+    I.ev_pool.push_back(e);
+  }
+  *a = I.ev_pool[I.ev_used++];
+  *b = I.ev_pool[I.ev_used++];
+}
+
+void DeviceModule::FlushTimes() {
+  if (!impl_) return;
+  Impl &I = *impl_;
+  if (I.pending.empty() && !I.acc_zeroed) return;
+  HIP_CHECK(hipStreamSynchronize(S(stream_)));
+  for (const Impl::Pending &p : I.pending) *p.dst += ElapsedMs(p.a, p.b) * 1e-3;
+  I.pending.clear();
+  I.ev_used = 0;
+  if (I.acc_zeroed) {
+    unsigned long long v[2] = {0, 0};
+    HIP_CHECK(hipMemcpy(v, I.acc.p, 16, hipMemcpyDeviceToHost));
+    times_.score_cells += v[0];
+    I.acc_zeroed = false;
+  }
+}
+
+void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n, uint32_t q_first,
+                         uint32_t q_end, const std::vector<uint32_t> &counts,
+                         const std::vector<uint64_t> &offsets, uint32_t base,
+                         const GapConfig &gap, uint32_t *score, uint32_t *end, const ScoreSegment *next) {
+  Impl &I = *impl_;
+  if (n == 0) return;
+  if (gap.ext > 0) throw Error("positive gap extension score is not supported");
+  const Layout lay = ChooseLayout(q->L, base);
+  // packed int16 path (two candidates per lane) whenever every value fits
+  int max_abs = 0;
+  for (int v : I.h_matrix) max_abs = std::max(max_abs, v < 0 ? -v : v);
+  // encoding: f16 pairs when every score fits the exact-integer range of f16,
+  // else int16 pairs, else int32 (GHOSTM_K2=int32|int16|f16 restricts the choice)
+  const char *force = getenv("GHOSTM_K2");
+  const int64_t bound = (int64_t)q->L * max_abs;
+  const bool packed = ScorePacked(I.h_matrix, q->L, base, gap);
+  // f16 is exact below 2048; beyond that it runs with a guard and the int16
+  // kernel re-scores the (rare) candidates whose best reaches it
+  const bool half = packed && !(force && strcmp(force, "int16") == 0);
+  // the column-framed f16 kernel (k_score16f) holds values up to best + the
+  // largest frame, (steps + 1) * ext_pen; GHOSTM_K2=f16plain keeps k_score16<S, true>
+  const int64_t sigma_max = (int64_t)(base + lay.G) * (-gap.ext);
+  const bool framed = half && sigma_max <= 1000 && !(force && strcmp(force, "f16plain") == 0);
+  int guard = framed ? (bound + sigma_max < 2048 ? 0 : (int)(2040 - sigma_max)) : (bound < 2048 ? 0 : 2000);
+  if (half && getenv("GHOSTM_K2_GUARD")) guard = atoi(getenv("GHOSTM_K2_GUARD"));  // tests: force re-scores
+  const uint32_t per_block = ScorePerBlock(q, base, gap);
+  // tasks: prepared for this range by the previous Score() call, else built
+  // and uploaded here
+  const kern::ScoreTask *dtasks = nullptr;
+  size_t ntasks = 0;
+  for (const auto &p : I.prepared)
+    if (p.cand_begin == cand_begin && p.n == n && p.per_block == per_block) {
+      dtasks = I.tasks_all.as<kern::ScoreTask>() + p.off;
+      ntasks = p.count;
+    }
+  if (!dtasks) {
+    std::vector<kern::ScoreTask> tasks;
+    BuildScoreTasks(cand_begin, n, q_first, q_end, counts, offsets, per_block, &tasks);
+    I.tasks.Reserve(tasks.size() * sizeof(kern::ScoreTask));
+    HIP_CHECK(hipMemcpyAsync(I.tasks.p, tasks.data(), tasks.size() * sizeof(kern::ScoreTask),
+                             hipMemcpyHostToDevice, S(stream_)));
+    dtasks = I.tasks.as<kern::ScoreTask>();
+    ntasks = tasks.size();
+  }
   I.score_out.Reserve(n * 4);
   I.end_out.Reserve(n * 4);
-  HIP_CHECK(hipMemcpyAsync(I.tasks.p, tasks.data(), tasks.size() * sizeof(kern::ScoreTask),
-                           hipMemcpyHostToDevice, S(stream_)));
   kern::ScoreArgs a{};
   a.qseq = q->seq.as<uint8_t>();
   a.L = q->L;
@@ -581,7 +667,7 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
   a.mat = I.mat_k2.as<int>();
   a.cand_qid = I.cand_qid.as<uint32_t>();
   a.cand_start = I.cand_start.as<uint32_t>();
-  a.tasks = I.tasks.as<kern::ScoreTask>();
+  a.tasks = dtasks;
   a.base = base;
   a.extend = gap.extend;
   a.open = gap.open;
@@ -589,9 +675,15 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
   a.score_out = I.score_out.as<uint32_t>();
   a.end_out = I.end_out.as<uint32_t>();
   a.out_base = cand_begin;
+  // nothing read back (device merge, no guard): no host wait after K2; the
+  // cell count accumulates on the device and the launch time is resolved later
+  // (off by default: measured slower on the box, 476 -> 570 ms/step, with the
+  // host waiting once per segment instead of after K2; GHOSTM_K2_NOWAIT=1 enables)
+  static const bool nowait = getenv("GHOSTM_K2_NOWAIT") && !strcmp(getenv("GHOSTM_K2_NOWAIT"), "1");
+  const bool deferred = nowait && !score && !end && !(half && guard);
   I.counters.Reserve(32);
-  HIP_CHECK(hipMemsetAsync(I.counters.p, 0, 32, S(stream_)));
-  a.cells = I.counters.as<unsigned long long>();
+  if (!deferred) HIP_CHECK(hipMemsetAsync(I.counters.p, 0, 32, S(stream_)));
+  a.cells = deferred ? AccCells(I, S(stream_)) : I.counters.as<unsigned long long>();
   uint32_t *guard_count = reinterpret_cast<uint32_t *>(I.counters.as<unsigned long long>() + 2);
   if (half && guard) {
     I.guard_list.Reserve((size_t)n * 8);
@@ -601,8 +693,10 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
   }
   const size_t lds = packed ? (size_t)kern::kScoreQmax * kern::kProfRows16 * (lay.Lpad + 8) * 2
                             : (size_t)kern::kScoreQmax * kern::kProfRows * (lay.Lpad + 4) * 4;
-  HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
-  const dim3 grid((uint32_t)tasks.size()), block(kern::kScoreBlock);
+  hipEvent_t e0 = I.ev0, e1 = I.ev1;
+  if (deferred) NewEventPair(I, &e0, &e1);
+  HIP_CHECK(hipEventRecord(e0, S(stream_)));
+  const dim3 grid((uint32_t)ntasks), block(kern::kScoreBlock);
   if (packed) {
     switch (lay.S) {
       case 32:
@@ -629,7 +723,21 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
     }
   }
   HIP_CHECK(hipGetLastError());
-  HIP_CHECK(hipEventRecord(I.ev1, S(stream_)));
+  HIP_CHECK(hipEventRecord(e1, S(stream_)));
+  times_.score_launches += 1;
+  times_.score_launches_packed += packed ? 1 : 0;
+  times_.score_launches_half += half ? 1 : 0;
+  times_.score_launches_framed += framed ? 1 : 0;
+  // the next segment's tasks, built on the host while K2 runs
+  I.prepared.clear();
+  I.next_tasks.clear();
+  if (next && next->n) BuildScoreTasks(next->cand_begin, next->n, next->q_first, next->q_end, counts, offsets,
+                                       per_block, &I.next_tasks);
+  if (deferred) {
+    I.pending.push_back({e0, e1, &times_.score});
+    UploadNextTasks(next, per_block);  // stream-ordered after this K2
+    return;
+  }
   if (score) HIP_CHECK(hipMemcpyAsync(score, I.score_out.p, n * 4, hipMemcpyDeviceToHost, S(stream_)));
   if (end) HIP_CHECK(hipMemcpyAsync(end, I.end_out.p, n * 4, hipMemcpyDeviceToHost, S(stream_)));
   unsigned long long cells = 0;
@@ -649,6 +757,7 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
     I.tasks.Reserve(redo.size() * sizeof(kern::ScoreTask));
     HIP_CHECK(hipMemcpy(I.tasks.p, redo.data(), redo.size() * sizeof(kern::ScoreTask), hipMemcpyHostToDevice));
     kern::ScoreArgs r = a;
+    r.tasks = I.tasks.as<kern::ScoreTask>();
     r.guard = 0;
     r.cells = I.counters.as<unsigned long long>() + 3;  // not counted twice
     const dim3 rgrid(nguard);
@@ -663,11 +772,18 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
     HIP_CHECK(hipStreamSynchronize(S(stream_)));
     times_.score_rechecks += nguard;
   }
-  times_.score_launches += 1;
-  times_.score_launches_packed += packed ? 1 : 0;
-  times_.score_launches_half += half ? 1 : 0;
-  times_.score_launches_framed += framed ? 1 : 0;
   times_.score_cells += cells;
+  UploadNextTasks(next, per_block);
+}
+
+// after the current K2 has finished (its tasks may live in tasks_all)
+void DeviceModule::UploadNextTasks(const ScoreSegment *next, uint32_t per_block) {
+  Impl &I = *impl_;
+  if (!next || I.next_tasks.empty()) return;
+  I.tasks_all.Reserve(I.next_tasks.size() * sizeof(kern::ScoreTask));
+  HIP_CHECK(hipMemcpyAsync(I.tasks_all.p, I.next_tasks.data(), I.next_tasks.size() * sizeof(kern::ScoreTask),
+                           hipMemcpyHostToDevice, S(stream_)));
+  I.prepared.push_back({next->cand_begin, next->n, 0, (uint32_t)I.next_tasks.size(), per_block});
 }
 
 // K3 launch: the key formulation when its field widths hold (len < 511,
@@ -855,7 +971,8 @@ void DeviceModule::MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, 
   m.sel_sid = I.sel_sid.as<uint32_t>();
   m.tb_qid = I.tb_qid.as<uint32_t>();
   m.tb_end = I.tb_end.as<uint32_t>();
-  HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
+  hipEvent_t m0 = I.ev0, m1 = I.ev1;
+  HIP_CHECK(hipEventRecord(m0, S(stream_)));
   // K4: one wave per name group (keys in LDS) for -b up to kMergeBest, else
   // one thread per group; GHOSTM_K4=thread|wave forces one (tests)
   bool wave = best >= 1 && best <= kern::kMergeBest;
@@ -874,8 +991,8 @@ void DeviceModule::MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, 
   times_.merge_launches += 1;
   times_.merge_launches_wave += wave ? 1 : 0;
   HIP_CHECK(hipGetLastError());
-  HIP_CHECK(hipEventRecord(I.ev1, S(stream_)));
-  times_.merge += ElapsedMs(I.ev0, I.ev1) * 1e-3;
+  HIP_CHECK(hipEventRecord(m1, S(stream_)));
+  times_.merge += ElapsedMs(m0, m1) * 1e-3;
 
   // K3 over the slots (empty slots carry qid 0xFFFFFFFF and are skipped)
   kern::TbArgs a{};
