@@ -630,9 +630,12 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
   const bool half = packed && !(force && strcmp(force, "int16") == 0);
   // the column-framed f16 kernel (k_score16f) holds values up to best + the
   // largest frame, (steps + 1) * ext_pen; GHOSTM_K2=f16plain keeps k_score16<S, true>
-  const int64_t sigma_max = (int64_t)(base + lay.G) * (-gap.ext);
+  // (the frame before a window's first END starts at -2040 + G * ext_pen)
+  const int64_t sigma_max = (int64_t)(base + 2 * lay.G) * (-gap.ext);
   const bool framed = half && sigma_max <= 1000 && !(force && strcmp(force, "f16plain") == 0);
-  int guard = framed ? (bound + sigma_max < 2048 ? 0 : (int)(2040 - sigma_max)) : (bound < 2048 ? 0 : 2000);
+  // framed: values stay exact and the -2040-based frame stays below the
+  // post-END one while best + sigma_max < 2040; beyond, the guard flags them
+  int guard = framed ? (bound + sigma_max < 2040 ? 0 : (int)(2040 - sigma_max)) : (bound < 2048 ? 0 : 2000);
   if (half && getenv("GHOSTM_K2_GUARD")) guard = atoi(getenv("GHOSTM_K2_GUARD"));  // tests: force re-scores
   const uint32_t per_block = ScorePerBlock(q, base, gap);
   // tasks: prepared for this range by the previous Score() call, else built

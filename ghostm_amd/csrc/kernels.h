@@ -574,6 +574,7 @@ constexpr int kScoreBlock = 256;
 constexpr int kScoreQmax = 4;
 constexpr uint32_t kProfRows = 26;
 constexpr uint32_t kProfRows16 = 32;  // packed kernels: one profile row per residue code
+constexpr uint32_t kFillCode = 26;     // k_score16f: profile row of the columns before the window
 constexpr uint32_t kDbFrontPad = 64;  // END bytes in front of the DB residues (device.hip)
 
 struct ScoreTask {
@@ -1056,8 +1057,9 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
   for (uint32_t e = threadIdx.x; e < total; e += kScoreBlock) {
     const uint32_t slot = e / per_slot, rem = e - slot * per_slot;
     const uint32_t c = rem / a.Lpad, r = rem - c * a.Lpad;
-    int v = kNeg16;
-    if (r >= a.pad) v = (c < 25 ? a.mat[c * 32 + a.qseq[(size_t)(t.q_first + slot) * a.L + (r - a.pad)]] : 0) + extp;
+    int v = kNeg16;  // padding rows; row kFillCode: the columns before the window
+    if (r >= a.pad && c != kFillCode)
+      v = (c < 25 ? a.mat[c * 32 + a.qseq[(size_t)(t.q_first + slot) * a.L + (r - a.pad)]] : 0) + extp;
     s_prof16[(slot * kProfRows16 + c) * RS + r] = C::Encode(v);
   }
   __syncthreads();
@@ -1094,29 +1096,47 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
   const hf2 KOE = HF(C::Pair(a.open - a.ext));
   const hf2 NEXT = HF(C::Pair(a.ext));
 
+  // Frame bases: until the window's first true END the frame is based near
+  // -2040 (sigma(j) = -2040 + (G + j) * ext_pen), so every value there is
+  // negative; that END restarts it at 0, above every stale E, and max3(E, oE,
+  // sigma) resets E by itself. Only a second true END needs the explicit reset.
+  // The fill columns before the window read profile row kFillCode (all
+  // kNeg16): the state stays at real 0 through them with no restart, so the
+  // frame is one function of the column for every lane of a group.
+  const uint32_t NEGF = C::Pair(-30000);  // F into the first row of a group: real < 0
+  uint32_t sig = C::Pair(-2040 + ((int)a.G - (int)i) * extp);  // sigma(-i), this lane's first column
   uint32_t H[S], E[S];
+  const uint32_t sig_prev = C::Pair(-2040 + ((int)a.G - (int)i - 1) * extp);
 #pragma unroll
-  for (int k = 0; k < S; ++k) { H[k] = 0; E[k] = EXTP; }
-  uint32_t sig = EXTP;                   // frame of the current column (real 0), per half
+  for (int k = 0; k < S; ++k) { H[k] = sig_prev; E[k] = sig; }
+  uint32_t seen = 0;                     // halves past a true END (0xFFFF)
   uint32_t best = 0, col = 0;
   uint32_t jj = ((0u - i) & 0xFFFFu) * 0x10001u;
   uint32_t nend = 0;
-  uint32_t hout = 0, fout = 0, hprev = 0;
-  uint32_t prev_end = 0xFFFFFFFFu;
+  // what the lane below reads before this lane's first column: real 0 in its
+  // frame for H (sigma(-i - 1)), and a real F below 0
+  uint32_t hout = sig_prev, fout = NEGF, hprev = sig_prev;
+  uint32_t prev_end = 0;
   uint32_t c0A = dbp[xA], c0B = dbp[xB], c1A = dbp[xA + 1], c1B = dbp[xB + 1];
   const uint32_t steps = a.base + a.G - 1;
   const uint32_t wA_ = vA ? wA : 0u, wB_ = vB ? wB : 0u;
-  auto column = [&](uint32_t step, auto tested_c) {
-    constexpr bool tested = decltype(tested_c)::value;
+  auto column = [&](uint32_t step, auto tested_c, auto fill_c) {
+    constexpr bool tested = decltype(tested_c)::value, in_fill = decltype(fill_c)::value;
     uint32_t hin = ShiftUp(hout), fin = ShiftUp(fout);
-    if (i == 0) { hin = sig; fin = 0; }  // real 0 for H; any real F <= 0 will do
+    if (i == 0) { hin = sig; fin = NEGF; }  // real 0 for H; any real F <= 0 will do
     const uint32_t diag0 = hprev;
     hprev = hin;
     uint32_t rA = c0A, rB = c0B;
+    uint32_t fillm = 0;  // both halves: this lane's column lies before the window
     if constexpr (tested) {
       const uint32_t j = step - i;
       rA = j < wA_ ? rA : kSeqEnd;
       rB = j < wB_ ? rB : kSeqEnd;
+      if constexpr (in_fill) {
+        fillm = (int)j < 0 ? 0xFFFFFFFFu : 0u;
+        rA = fillm ? kFillCode : rA;
+        rB = fillm ? kFillCode : rB;
+      }
     }
     c0A = c1A;
     c0B = c1B;
@@ -1124,15 +1144,19 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
     c1A = colp[xA];
     c1B = colp[xB];
     const uint32_t rr = rA | (rB << 16);
-    const uint32_t end = PkSign(PkAddU16(rr, 0x7FE77FE7u));
+    uint32_t end = PkSign(PkAddU16(rr, 0x7FE77FE7u));  // codes >= 25
+    if constexpr (in_fill) end &= ~fillm;
     const hf2 m = HF(C::kOne & ~prev_end);
     prev_end = end;
-    // the next column's frame: one step on, or restarted after END
+    // the next column's frame: one step on, or restarted at 0 after a true END;
+    // E needs the explicit reset only where the half already met one
+    const uint32_t reset = end & seen;
+    seen |= end;
     const uint32_t zn = BfiV(end, EXTP, W(HF(sig) + HF(EXTP)));
     const hf2 Z1 = HF(zn);
     const char *pA = reinterpret_cast<const char *>(s_prof16) + MadU24(rA, RS2, baseA2);
     const char *pB = reinterpret_cast<const char *>(s_prof16) + MadU24(rB, RS2, baseB2);
-    uint32_t diag = diag0, F = fin, cm = 0;
+    uint32_t diag = diag0, F = fin, cm = sig;
 #pragma unroll
     for (int k = 0; k < S; k += 8) {
       const uint4 qa = *reinterpret_cast<const uint4 *>(pA + 2 * k);
@@ -1168,25 +1192,25 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
     }
     hout = H[S - 1];
     fout = F;
-    // END halves: E restarts at real 0 in the new frame (H needs nothing: the
-    // next column masks the diagonal, and F restarts from the lane above)
-    if (__builtin_amdgcn_ballot_w64(end != 0)) {  // wave-uniform: a real branch
+    // halves to reset: E restarts at real 0 in the new frame (H needs nothing:
+    // the next column masks the diagonal, and F restarts from the lane above)
+    if (__builtin_amdgcn_ballot_w64(reset != 0)) {  // wave-uniform: a real branch
 #pragma unroll
-      for (int k = 0; k < S; ++k) E[k] = BfiV(end, zn, E[k]);
+      for (int k = 0; k < S; ++k) E[k] = BfiV(reset, zn, E[k]);
     }
     const uint32_t cmr = W(HF(cm) - HF(sig));  // real column maximum (>= 0 off END)
-    const uint32_t keep = PkSign(PkSubI16(cmr, best)) | end;
+    const uint32_t keep = PkSign(PkSubI16(cmr, best)) | end | fillm;
     best = BfiV(keep, best, cmr);
     col = BfiV(keep, col, jj);
     jj = PkAddU16(jj, 0x00010001u);
-    nend = PkAddU16(nend, end);
+    nend = PkAddU16(nend, end | fillm);
     sig = zn;
   };
   const uint32_t fill = min(a.G - 1, steps);
   uint32_t step = 0;
-  for (; step < fill; ++step) column(step, std::true_type{});
-  for (; step < a.base; ++step) column(step, std::false_type{});
-  for (; step < steps; ++step) column(step, std::true_type{});
+  for (; step < fill; ++step) column(step, std::true_type{}, std::true_type{});
+  for (; step < a.base; ++step) column(step, std::false_type{}, std::false_type{});
+  for (; step < steps; ++step) column(step, std::true_type{}, std::false_type{});
   const uint32_t ncolsA = steps - ((0x10000u - (nend & 0xFFFFu)) & 0xFFFFu);
   const uint32_t ncolsB = steps - ((0x10000u - (nend >> 16)) & 0xFFFFu);
   int BA = C::Decode(best & 0xFFFFu), CA = (int)(col & 0xFFFFu);
