@@ -682,7 +682,8 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
   // cell count accumulates on the device and the launch time is resolved later
   // (off by default: measured slower on the box, 476 -> 570 ms/step, with the
   // host waiting once per segment instead of after K2; GHOSTM_K2_NOWAIT=1 enables)
-  static const bool nowait = getenv("GHOSTM_K2_NOWAIT") && !strcmp(getenv("GHOSTM_K2_NOWAIT"), "1");
+  const char *nw = getenv("GHOSTM_K2_NOWAIT");
+  const bool nowait = nw && !strcmp(nw, "1");
   const bool deferred = nowait && !score && !end && !(half && guard);
   I.counters.Reserve(32);
   if (!deferred) HIP_CHECK(hipMemsetAsync(I.counters.p, 0, 32, S(stream_)));

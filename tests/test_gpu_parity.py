@@ -180,7 +180,7 @@ def test_reference_gpu_batching_rule(dataset):
     lib.FreeGpu()
 
 
-@pytest.mark.parametrize("kind", ["int32", "int16", "f16plain", "k3_int32", "k1_merge"])
+@pytest.mark.parametrize("kind", ["int32", "int16", "f16plain", "k2_nowait", "k3_int32", "k1_merge"])
 @pytest.mark.parametrize("ds,var,opts", [("syn_small", "default", []), ("syn_short", "default", []),
                                          ("syn_small", "r64_pam250", ["-r", "64", "-M", cases.PAM250, "-y", "2"])])
 def test_forced_score_encoding_matches_golden(kind, ds, var, opts, dataset, golden, tmp_path):
@@ -189,7 +189,8 @@ def test_forced_score_encoding_matches_golden(kind, ds, var, opts, dataset, gold
     scores may exceed int16. Forced with GHOSTM_K2 each reproduces the golden."""
     d = dataset(ds)
     env = ({"GHOSTM_K3": "int32"} if kind == "k3_int32" else
-           {"GHOSTM_K1": "merge"} if kind == "k1_merge" else {"GHOSTM_K2": kind})
+           {"GHOSTM_K1": "merge"} if kind == "k1_merge" else
+           {"GHOSTM_K2_NOWAIT": "1"} if kind == "k2_nowait" else {"GHOSTM_K2": kind})
     text, st = _gpu_text(d, opts, env, str(tmp_path / "g.out"))
     (tmp_path / "g.out").write_bytes(text)
     assert cases.sha256(str(tmp_path / "g.out")) == golden["aln"][f"{ds}/{var}"]["sha256"]
@@ -198,6 +199,8 @@ def test_forced_score_encoding_matches_golden(kind, ds, var, opts, dataset, gold
         assert st["traceback_launches_key"] == 0
     elif kind == "k1_merge":
         assert st["seed_runs_hash"] == 0
+    elif kind == "k2_nowait":  # K2 launches without a host wait, timings resolved at the end
+        assert st["score_launches_framed"] == st["score_launches"] > 0 and st["score_cells"] > 0
     elif kind == "f16plain":
         assert st["score_launches_half"] == st["score_launches"] > 0 and st["score_launches_framed"] == 0
     else:
