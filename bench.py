@@ -205,7 +205,7 @@ def main() -> None:
     k = args.steps
     per = {key: v / k for key, v in st_acc.items()}
     cpu = None
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu:  # the CPU baseline is an N=1 figure
         cpu = cpu_baseline(workdir, args.cpu_sample, args.db_residues, first, preset["seed"], aln_args)
     if rank == 0:
         score_t = per["seconds_score"] / max(1, per["score_launches"])
