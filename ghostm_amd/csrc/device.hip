@@ -165,12 +165,15 @@ void DeviceModule::Bind(int device) {
   HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_seed<512, 8192, false>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 8192 * 4));
   const int scan_lds = (int)kScanLds;
-#define GHOSTM_SCAN_ATTR(SS, HH, EE)                                                 \
-  HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_tb_scan<SS, HH, EE>,           \
+#define GHOSTM_SCAN_ATTR(SS, HH, EE, FF)                                             \
+  HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_tb_scan<SS, HH, EE, FF>,       \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, scan_lds));
-#define GHOSTM_SCAN_ATTR2(SS, HH) GHOSTM_SCAN_ATTR(SS, HH, true) GHOSTM_SCAN_ATTR(SS, HH, false)
+#define GHOSTM_SCAN_ATTR2(SS, HH) GHOSTM_SCAN_ATTR(SS, HH, true, false) GHOSTM_SCAN_ATTR(SS, HH, false, false)
   GHOSTM_SCAN_ATTR2(32, true) GHOSTM_SCAN_ATTR2(32, false) GHOSTM_SCAN_ATTR2(16, true)
   GHOSTM_SCAN_ATTR2(16, false) GHOSTM_SCAN_ATTR2(8, true) GHOSTM_SCAN_ATTR2(8, false)
+  GHOSTM_SCAN_ATTR(32, true, true, true) GHOSTM_SCAN_ATTR(32, true, false, true)
+  GHOSTM_SCAN_ATTR(16, true, true, true) GHOSTM_SCAN_ATTR(16, true, false, true)
+  GHOSTM_SCAN_ATTR(8, true, true, true) GHOSTM_SCAN_ATTR(8, true, false, true)
 #undef GHOSTM_SCAN_ATTR2
 #undef GHOSTM_SCAN_ATTR
   {
@@ -826,6 +829,10 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
   const bool scan = !scan_off && n > 0 && scan_gaps && hmax < 30000 && a.base < 65536;
   if (scan) {
     const bool half = hmax < 2048 && !(scan_env && strcmp(scan_env, "int16") == 0);
+    // the column-framed f16 scan: values up to best + (window + 2G) * ext_pen
+    // must stay exact (GHOSTM_K3_SCAN=f16plain keeps the unframed one)
+    const int64_t scan_sigma = (int64_t)(a.base + 2 * lay.G) * (-a.ext);
+    const bool framed = half && hmax + scan_sigma < 2048 && !(scan_env && strcmp(scan_env, "f16plain") == 0);
     const uint32_t NB = kern::kSortBins;
     I.tb_width.Reserve((size_t)n * 4);
     I.tb_ncols.Reserve((size_t)n * 4);
@@ -891,13 +898,16 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
     // exact windows (cut at the subject's start) need the DB's subject table
     const bool exact = subj != nullptr;
     sa.best_out = I.tb_best.as<uint32_t>();
-#define GHOSTM_SCAN1(SS, HH, EE) \
-  hipLaunchKernelGGL((kern::k_tb_scan<SS, HH, EE>), dim3(blocks), dim3(kern::kScanBlock), kScanLds, S(stream_), sa)
-#define GHOSTM_SCAN(SS)                            \
-  if (half && exact) GHOSTM_SCAN1(SS, true, true); \
-  else if (half) GHOSTM_SCAN1(SS, true, false);    \
-  else if (exact) GHOSTM_SCAN1(SS, false, true);   \
-  else GHOSTM_SCAN1(SS, false, false);
+#define GHOSTM_SCAN1(SS, HH, EE, FF)                                                                          \
+  hipLaunchKernelGGL((kern::k_tb_scan<SS, HH, EE, FF>), dim3(blocks), dim3(kern::kScanBlock), kScanLds, S(stream_), \
+                     sa)
+#define GHOSTM_SCAN(SS)                                          \
+  if (framed && exact) GHOSTM_SCAN1(SS, true, true, true);       \
+  else if (framed) GHOSTM_SCAN1(SS, true, false, true);          \
+  else if (half && exact) GHOSTM_SCAN1(SS, true, true, false);   \
+  else if (half) GHOSTM_SCAN1(SS, true, false, false);           \
+  else if (exact) GHOSTM_SCAN1(SS, false, true, false);          \
+  else GHOSTM_SCAN1(SS, false, false, false);
     switch (lay.S) {
       case 32: GHOSTM_SCAN(32); break;
       case 16: GHOSTM_SCAN(16); break;

@@ -2065,16 +2065,27 @@ __global__ void k_rev_codes(const uint8_t *qseq, uint32_t nq, uint32_t L, uint32
 // halves at dword (a * 26 + b) * kPairStride + q; the per-column pair base plus
 // the row's 4q is one SDWA add per row, and one ds_read_b32 gives both hits'
 // profile values, with no v_perm.
-template <int S, bool HALF, bool EXACT>
+// FRAMED (f16 only): the column frame of k_score16f, based at 0 with no restart:
+// a half meeting END is dead (the reference breaks there), so its later values
+// are never read, and the fill columns before the window (END-coded) read an
+// all-kNeg row, which keeps the state at real 0 with no reset. No END penalty
+// switching, no diagonal mask: 6 packed ops per row pair instead of 7.
+template <int S, bool HALF, bool EXACT, bool FRAMED = false>
 __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
   using C = Cells<HALF>;
+  static_assert(!FRAMED || HALF, "the frame is an f16 kernel");
   extern __shared__ __attribute__((aligned(16))) uint32_t s_pair[];
   uint32_t *s_hist = s_pair + kPairWords;
+  const int extp = -a.ext;
   for (uint32_t e = threadIdx.x; e < kPairWords; e += kScanBlock) {
     const uint32_t pr = e / kPairStride, q = e - pr * kPairStride;
     const uint32_t ca = pr / kPairCodes, cb = pr - ca * kPairCodes;
-    const int va = q == kPadCode ? kNeg16 : (ca < 25 && q < 25 ? a.mat[ca * 32 + q] : 0);
-    const int vb = q == kPadCode ? kNeg16 : (cb < 25 && q < 25 ? a.mat[cb * 32 + q] : 0);
+    int va = q == kPadCode ? kNeg16 : (ca < 25 && q < 25 ? a.mat[ca * 32 + q] : 0);
+    int vb = q == kPadCode ? kNeg16 : (cb < 25 && q < 25 ? a.mat[cb * 32 + q] : 0);
+    if constexpr (FRAMED) {
+      va = (q == kPadCode || ca == kSeqEnd) ? kNeg16 : va + extp;
+      vb = (q == kPadCode || cb == kSeqEnd) ? kNeg16 : vb + extp;
+    }
     s_pair[e] = (uint32_t)(unsigned short)C::Encode(va) | (uint32_t)(unsigned short)C::Encode(vb) << 16;
   }
   for (uint32_t b = threadIdx.x; b < kSortBins; b += kScanBlock) s_hist[b] = 0;
@@ -2121,11 +2132,15 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
       }
     }
     uint32_t H[S], E[S];
+    // FRAMED: sigma(j) = (G + j) * ext_pen, this lane starts at column -i
+    const uint32_t EXTP = Cells<true>::Pair(extp);
+    uint32_t sig = FRAMED ? Cells<true>::Pair(((int)a.G - (int)i) * extp) : 0u;
+    const uint32_t sig_prev = FRAMED ? Cells<true>::Pair(((int)a.G - (int)i - 1) * extp) : 0u;
 #pragma unroll
-    for (int k = 0; k < S; ++k) { H[k] = 0; E[k] = 0; }
+    for (int k = 0; k < S; ++k) { H[k] = sig_prev; E[k] = sig; }
     uint32_t best = 0, col = 0;                 // packed halves
     uint32_t dead = (wA ? 0u : 0x0000FFFFu) | (wB ? 0u : 0xFFFF0000u);
-    uint32_t hout = 0, fout = 0, hprev = 0, prev_end = 0xFFFFFFFFu;
+    uint32_t hout = sig_prev, fout = 0, hprev = sig_prev, prev_end = FRAMED ? 0u : 0xFFFFFFFFu;
     const uint32_t ww = wA | (wB << 16);                     // packed windows
     uint32_t jj = ((0u - i) & 0xFFFFu) * 0x10001u;           // packed column j (mod 2^16)
     const uint32_t clA = (wA ? wA : 1u) - 1, clB = (wB ? wB : 1u) - 1;
@@ -2154,7 +2169,7 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
       constexpr bool run = decltype(run_c)::value;
       const int j = (int)step - (int)i;
       uint32_t hin = ShiftUp(hout), fin = ShiftUp(fout);
-      if (i == 0) { hin = 0; fin = 0; }
+      if (i == 0) { hin = sig; fin = 0; }  // framed 0 is a real F <= 0
       const uint32_t diag0 = hprev;
       hprev = hin;
       const uint32_t rA = nA, rB = nB;
@@ -2171,25 +2186,46 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
         // END halves: codes are 0..25 with END = 25 the largest
         end = PkSign(PkAddU16(rA | (rB << 16), 0x7FE77FE7u));
         if (j >= 0) dead |= end;                  // the reference breaks at END
-        st = cell.At(end, prev_end);
-        prev_end = end;
+        if constexpr (!FRAMED) {
+          st = cell.At(end, prev_end);
+          prev_end = end;
+        }
       }
+      const hf2 Z1 = HF(W(HF(sig) + HF(EXTP)));  // FRAMED: the next column's frame
+      const hf2 KOE = HF(Cells<true>::Pair(a.open - a.ext)), NEXT = HF(Cells<true>::Pair(a.ext));
       const uint32_t cbase = MadU24(min(rA, kPairCodes - 1), kPairCodes * kPairStride * 4,
                                     MulU24(min(rB, kPairCodes - 1), kPairStride * 4));
       const char *tp = reinterpret_cast<const char *>(s_pair) + cbase;
       auto T = [&](int u) { return *reinterpret_cast<const uint32_t *>(tp + ((qoff[u >> 2] >> (8 * (u & 3))) & 0xFFu)); };
-      uint32_t diag = diag0, F = fin, cm = 0;
+      uint32_t diag = diag0, F = fin, cm = sig;
 #pragma unroll
       for (int k = 0; k < S; k += 8) {
         // the chunk's eight table reads issued together, then their sums
         uint32_t t[8], s[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) t[u] = T(k + u);
+        if constexpr (FRAMED) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) s[u] = C::Diag(u == 0 ? diag : H[k + u - 1], st.m, t[u]);
+          for (int u = 0; u < 8; ++u) s[u] = W(HF(u == 0 ? diag : H[k + u - 1]) + HF(t[u]));
+        } else {
+#pragma unroll
+          for (int u = 0; u < 8; ++u) s[u] = C::Diag(u == 0 ? diag : H[k + u - 1], st.m, t[u]);
+        }
         diag = H[k + 7];
+        if constexpr (FRAMED) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) C::Row(st, s[u], H[k + u], E[k + u], F);
+          for (int u = 0; u < 8; ++u) {
+            const hf2 h = __builtin_elementwise_maximum(__builtin_elementwise_maximum(HF(s[u]), HF(E[k + u])), HF(F));
+            H[k + u] = W(h);
+            const hf2 oE = h + KOE;
+            const hf2 G = __builtin_elementwise_maximum(HF(F), oE);
+            E[k + u] = W(__builtin_elementwise_maximum(__builtin_elementwise_maximum(HF(E[k + u]), oE), Z1));
+            F = W(G + NEXT);
+          }
+        } else {
+#pragma unroll
+          for (int u = 0; u < 8; ++u) C::Row(st, s[u], H[k + u], E[k + u], F);
+        }
         cm = C::Max3(C::Max3(H[k], H[k + 1], H[k + 2]), C::Max3(H[k + 3], H[k + 4], H[k + 5]),
                      C::Max3(H[k + 6], H[k + 7], cm));
         // the next chunk's table reads stay behind this one (register budget)
@@ -2200,6 +2236,10 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
       // strict first maximum per live half: best - cm < 0 iff cm > best. Live:
       // inside the window (j - w < 0) on run steps, else neither END nor dead
       const uint32_t live = run ? PkSign(PkSubI16(jj, ww)) : ~(end | dead);
+      if constexpr (FRAMED) {
+        cm = W(HF(cm) - HF(sig));  // real column maximum
+        sig = W(Z1);
+      }
       const uint32_t upd = PkSign(PkSubI16(best, cm)) & live;
       best = BfiV(upd, cm, best);
       col = BfiV(upd, jj, col);

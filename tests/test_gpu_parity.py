@@ -280,14 +280,15 @@ def test_wide_band_traceback_uses_key_kernel(dataset, golden, tmp_path):
     assert st["traceback_launches_key"] == st["traceback_launches"] > 0
 
 
-@pytest.mark.parametrize("mode", ["default", "int16", "0"])
+@pytest.mark.parametrize("mode", ["default", "f16plain", "int16", "0"])
 @pytest.mark.parametrize("ds,var,opts", [("syn_small", "default", []), ("syn_dna", "default", []),
                                          ("syn_chunks", "default", []), ("protein_testset", "y2", ["-y", "2"]),
                                          ("syn_small", "r64_pam250", ["-r", "64", "-M", cases.PAM250, "-y", "2"])])
 def test_traceback_scan_modes_match_golden(mode, ds, var, opts, dataset, golden, tmp_path):
     """Two-pass traceback (K3a scores-only scan, then the key DP over columns
-    0..j* in j*-sorted order) in its f16 and int16 encodings, and the single-pass
-    traceback (GHOSTM_K3_SCAN=0): each reproduces the golden output."""
+    0..j* in j*-sorted order) in its encodings (default: the column-framed f16
+    scan; f16plain, int16), and the single-pass traceback (GHOSTM_K3_SCAN=0):
+    each reproduces the golden output."""
     d = dataset(ds)
     env = {} if mode == "default" else {"GHOSTM_K3_SCAN": mode}
     text, st = _gpu_text(d, opts, env, str(tmp_path / "g.out"))
