@@ -841,6 +841,13 @@ __device__ inline uint32_t MadU24(uint32_t a, uint32_t b, uint32_t c) {
   return r;
 }
 
+// b wave-uniform (an SGPR operand, no per-call copy into a VGPR)
+__device__ inline uint32_t MadU24s(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(c));
+  return r;
+}
+
 __device__ inline uint32_t MulU24(uint32_t a, uint32_t b) {
   uint32_t r;
   asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
@@ -1086,12 +1093,19 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
     wB = a.base;
     if (offB + wB > a.dblen) wB = a.dblen - offB;
   }
-  const uint32_t baseA2 = (slotA * kProfRows16 * RS + i * S) * 2;
-  const uint32_t baseB2 = (slotB * kProfRows16 * RS + i * S) * 2;
+  // LDS byte addresses (32-bit, the profile's own base folded in once)
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) const u32x4 lds_u4;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char *)s_prof16;
+  const uint32_t baseA2 = lds0 + (slotA * kProfRows16 * RS + i * S) * 2;
+  const uint32_t baseB2 = lds0 + (slotB * kProfRows16 * RS + i * S) * 2;
   const uint8_t *dbp = a.db - kDbFrontPad;
   const uint32_t back = kDbFrontPad + a.dblen;
   const uint32_t xA = (vA ? offA + kDbFrontPad : back) - i, xB = (vB ? offB + kDbFrontPad : back) - i;
   const uint32_t RS2 = RS * 2;
+  // the padded DB as a raw buffer (gfx9 descriptor word 3; every access stays
+  // inside the padding, so the range is left open)
+  const __amdgpu_buffer_rsrc_t dbr = __builtin_amdgcn_make_buffer_rsrc((void *)dbp, 0, 0x7FFFFFFF, 0x00020000);
   const uint32_t EXTP = C::Pair(extp);
   const hf2 KOE = HF(C::Pair(a.open - a.ext));
   const hf2 NEXT = HF(C::Pair(a.ext));
@@ -1140,9 +1154,10 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
     }
     c0A = c1A;
     c0B = c1B;
-    const uint8_t *colp = dbp + step + 2;
-    c1A = colp[xA];
-    c1B = colp[xB];
+    // buffer loads: the lane's offset x in a VGPR, the column in the scalar
+    // offset, no per-column 64-bit address arithmetic
+    c1A = __builtin_amdgcn_raw_buffer_load_b8(dbr, xA, step + 2, 0);
+    c1B = __builtin_amdgcn_raw_buffer_load_b8(dbr, xB, step + 2, 0);
     const uint32_t rr = rA | (rB << 16);
     uint32_t end = PkSign(PkAddU16(rr, 0x7FE77FE7u));  // codes >= 25
     if constexpr (in_fill) end &= ~fillm;
@@ -1154,13 +1169,13 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
     seen |= end;
     const uint32_t zn = BfiV(end, EXTP, W(HF(sig) + HF(EXTP)));
     const hf2 Z1 = HF(zn);
-    const char *pA = reinterpret_cast<const char *>(s_prof16) + MadU24(rA, RS2, baseA2);
-    const char *pB = reinterpret_cast<const char *>(s_prof16) + MadU24(rB, RS2, baseB2);
+    lds_u4 *pA = (lds_u4 *)(uintptr_t)MadU24s(rA, RS2, baseA2);
+    lds_u4 *pB = (lds_u4 *)(uintptr_t)MadU24s(rB, RS2, baseB2);
     uint32_t diag = diag0, F = fin, cm = sig;
 #pragma unroll
     for (int k = 0; k < S; k += 8) {
-      const uint4 qa = *reinterpret_cast<const uint4 *>(pA + 2 * k);
-      const uint4 qb = *reinterpret_cast<const uint4 *>(pB + 2 * k);
+      const u32x4 qa = pA[k / 8];
+      const u32x4 qb = pB[k / 8];
       const uint32_t wa[4] = {qa.x, qa.y, qa.z, qa.w}, wb[4] = {qb.x, qb.y, qb.z, qb.w};
       // row u's profile pair (perm) and diagonal sum, formed from the previous
       // column's H[k + u - 1] before row u - 1 overwrites it
@@ -1209,6 +1224,11 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
   const uint32_t fill = min(a.G - 1, steps);
   uint32_t step = 0;
   for (; step < fill; ++step) column(step, std::true_type{}, std::true_type{});
+  // two columns per trip: the rotating registers (codes, diagonal) stay put
+  for (; step + 1 < a.base; step += 2) {
+    column(step, std::false_type{}, std::false_type{});
+    column(step + 1, std::false_type{}, std::false_type{});
+  }
   for (; step < a.base; ++step) column(step, std::false_type{}, std::false_type{});
   for (; step < steps; ++step) column(step, std::true_type{}, std::false_type{});
   const uint32_t ncolsA = steps - ((0x10000u - (nend & 0xFFFFu)) & 0xFFFFu);
