@@ -97,7 +97,52 @@ def cpu_baseline(root: str, nsample: int, db_res: int, first: int, seed: int = 4
             "kind": "reference" if use_ref else "port",
             "sample": f"first {nsample} queries of rank 0's workload vs the same {db_res / 1e6:g}M-residue DB "
                       f"({residues} residues, {dt:.1f} s, {what}, 1 thread)",
-            "bit_identical_to_gpu_on_sample": bool(same)}
+            "bit_identical_to_gpu_on_sample": bool(same), "residues": residues}
+
+
+def cpu_baseline_multi(root: str, nsample: int, db_res: int, first: int, residues: int, seed: int = 4,
+                       aln_args: list | None = None, procs: int | None = None) -> dict | None:
+    """SURVEY §8 d4's second CPU figure: the same sample on all host cores the job
+    may use. The reference aligner is single-threaded, so it runs as `procs`
+    processes over contiguous query ranges (queries are independent; the
+    concatenated outputs must equal the one-process output, checked here)."""
+    ref = os.path.join(REPO, "oracle", "_ref", "ghostm_ref")
+    port = os.path.join(REPO, "oracle", "_build", "ghostm_oracle")
+    exe = ref if os.path.exists(ref) else port
+    ghostm = os.path.join(REPO, "ghostm_amd", "bin", "ghostm")
+    # the box's CPU share is 16 (OMP_NUM_THREADS is set to it); os.cpu_count()
+    # there reports the whole machine
+    procs = procs or max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)),
+                                os.cpu_count() or 1))
+    sub = os.path.join(root, "sample")
+    parts = []
+    per = (nsample + procs - 1) // procs
+    for k in range(procs):
+        n = min(per, nsample - k * per)
+        if n <= 0:
+            break
+        d = os.path.join(sub, f"part{k}")
+        os.makedirs(d, exist_ok=True)
+        subprocess.run([ghostm, "synth", "-q", f"{d}/q.fa", "-n", str(n), "-N", str(db_res), "-s", str(seed),
+                        "-f", str(first + k * per)], check=True, capture_output=True)
+        subprocess.run([ghostm, "qry", "-i", f"{d}/q.fa", "-o", f"{d}/q", "-l", "300"], check=True,
+                       capture_output=True)
+        parts.append(d)
+    t0 = time.perf_counter()
+    running = [subprocess.Popen([exe, "aln", "-i", f"{d}/q", "-d", f"{root}/db", "-o", f"{d}/cpu.out"]
+                                + list(aln_args or []), stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+               for d in parts]
+    rcs = [p.wait() for p in running]
+    dt = time.perf_counter() - t0
+    if any(rcs):
+        return None
+    joined = b"".join(open(f"{d}/cpu.out", "rb").read() for d in parts)
+    single = open(f"{sub}/cpu.out", "rb").read()
+    return {"value": residues / dt, "unit": "query residues/s", "cores": len(parts),
+            "kind": "reference" if exe == ref else "port",
+            "sample": f"the cpu_baseline sample as {len(parts)} processes over contiguous query ranges "
+                      f"({dt:.1f} s)",
+            "identical_to_one_process": joined == single}
 
 
 def _device() -> int:
@@ -204,9 +249,11 @@ def main() -> None:
 
     k = args.steps
     per = {key: v / k for key, v in st_acc.items()}
-    cpu = None
+    cpu = cpu_multi = None
     if rank == 0 and world == 1 and not args.no_cpu:  # the CPU baseline is an N=1 figure
         cpu = cpu_baseline(workdir, args.cpu_sample, args.db_residues, first, preset["seed"], aln_args)
+        cpu_multi = cpu_baseline_multi(workdir, args.cpu_sample, args.db_residues, first,
+                                       cpu.pop("residues"), preset["seed"], aln_args)
     if rank == 0:
         score_t = per["seconds_score"] / max(1, per["score_launches"])
         score_cells = per["score_cells"] / max(1, per["score_launches"])
@@ -286,6 +333,7 @@ def main() -> None:
                 "output_host": per["seconds_output"],
             },
             "cpu_baseline": cpu,
+            "cpu_baseline_all_cores": cpu_multi,
         }
         print(json.dumps(out), flush=True)
     sess.close()
