@@ -333,8 +333,8 @@ static void LaunchSeed(const kern::SeedArgs &a, uint32_t items, hipStream_t s) {
 static void LaunchSeedHashClass(int cls, const kern::SeedArgs &a, uint32_t items, hipStream_t s) {
   if (items == 0) return;
   switch (cls) {
-    case 0:  // load <= 2/3: 24 KB, six workgroups per CU
-      hipLaunchKernelGGL((kern::k_seed_hash<256, 6144>), dim3(items), dim3(256), 6144 * 4, s, a);
+    case 0:
+      hipLaunchKernelGGL((kern::k_seed_hash<256, 8192>), dim3(items), dim3(256), 8192 * 4, s, a);
       break;
     case 1:  // load <= 2/3: 48 KB, three workgroups per CU
       hipLaunchKernelGGL((kern::k_seed_hash<512, 12288>), dim3(items), dim3(512), 12288 * 4, s, a);
