@@ -171,13 +171,14 @@ def main() -> None:
     ap.add_argument("--cpu-sample", type=int, default=2000)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--workdir", default=None)
+    ap.add_argument("--aln", default="", help="extra aln options appended to the preset's (e.g. '-l 64')")
     args = ap.parse_args()
     preset = PRESETS[args.preset]
     if args.queries is None:
         args.queries = preset["queries"]
     if args.db_residues is None:
         args.db_residues = preset["db"]
-    aln_args = list(preset["aln"])
+    aln_args = list(preset["aln"]) + args.aln.split()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

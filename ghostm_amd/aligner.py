@@ -49,13 +49,25 @@ class Aligner:
 
 
 class Session:
-    def __init__(self, argv: Sequence[str]):
+    """`shard=(rank, world)`: search only that shard of the query set (one process
+    per GPU, GhostmSessionCreateShard); rank-order concatenation of the shards'
+    outputs is the unsharded output."""
+
+    def __init__(self, argv: Sequence[str], shard: tuple[int, int] | None = None):
         lib = native.load()
         args = ["aln"] + list(argv)
         self._argv = native.argv_array(args)
-        self._h = lib.GhostmSessionCreate(len(args), self._argv)
+        if shard is None:
+            self._h = lib.GhostmSessionCreate(len(args), self._argv)
+        else:
+            self._h = lib.GhostmSessionCreateShard(len(args), self._argv, int(shard[0]), int(shard[1]))
         if not self._h:
             raise GhostmError(native.last_error())
+
+    def shard_range(self) -> tuple[int, int]:
+        b, e = ctypes.c_uint64(), ctypes.c_uint64()
+        native.load().GhostmSessionShardRange(self._h, ctypes.byref(b), ctypes.byref(e))
+        return b.value, e.value
 
     def run(self) -> None:
         if native.load().GhostmSessionRun(self._h) != 0:

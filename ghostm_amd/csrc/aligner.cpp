@@ -151,8 +151,70 @@ AlignerOptions ParseAlignerOptions(int argc, char **argv) {
   return o;
 }
 
+// WriteOutput's query length: the index of the last non-X residue + 1, at
+// least 1 (aligner.cpp:959-961); also the query's residue count for the metric
+static uint32_t QueryLength(const uint8_t *s, uint32_t L) {
+  uint32_t e = L - 1;
+  while (e > 0 && s[e] == kBaseX) --e;
+  return e + 1;
+}
+
+// ------------------------------------------------------------------ shards
+void ShardCuts(uint64_t n, const uint32_t *weight, const uint8_t *group_start, uint32_t world, uint64_t *cuts) {
+  if (world == 0) throw std::invalid_argument("world must be >= 1");
+  std::vector<uint64_t> prefix(n + 1, 0);
+  for (uint64_t i = 0; i < n; ++i) prefix[i + 1] = prefix[i] + weight[i];
+  const unsigned __int128 total = prefix[n];
+  cuts[0] = 0;
+  for (uint32_t r = 1; r < world; ++r) {
+    // first group start at or after the previous cut whose prefix weight
+    // reaches total * r / world (exact integer comparison)
+    uint64_t c = cuts[r - 1];
+    while (c < n && !((c == 0 || group_start[c]) && (unsigned __int128)prefix[c] * world >= total * r)) ++c;
+    cuts[r] = c;
+  }
+  cuts[world] = n;
+}
+
+// Keep only this shard's queries: the chunks' queries are cut into `world`
+// contiguous ranges of about equal residues, at name-group starts (groups never
+// span chunks: the reference merges per chunk, aligner.cpp:697-700).
+void Session::ApplyShard(uint32_t rank, uint32_t world) {
+  std::vector<uint32_t> weight;
+  std::vector<uint8_t> start;
+  for (const QueryData &q : queries_) {
+    const QueryChunk &c = q.chunk;
+    for (uint32_t i = 0; i < c.nseq; ++i) {
+      weight.push_back(QueryLength(&c.seq[(size_t)i * c.L], c.L));
+      start.push_back(i == 0 || c.names[i] != c.names[i - 1]);
+    }
+  }
+  std::vector<uint64_t> cuts(world + 1);
+  ShardCuts(weight.size(), weight.data(), start.data(), world, cuts.data());
+  const uint64_t lo = cuts[rank], hi = cuts[rank + 1];
+  shard_begin_ = lo;
+  shard_end_ = hi;
+  std::vector<QueryData> kept;
+  uint64_t at = 0;  // index of the chunk's first query over the loaded chunks
+  for (QueryData &q : queries_) {
+    QueryChunk &c = q.chunk;
+    const uint64_t chunk_end = at + c.nseq;
+    const uint64_t b = std::max<uint64_t>(lo, at), e = std::min<uint64_t>(hi, chunk_end);
+    if (b < e) {
+      const uint32_t i0 = (uint32_t)(b - at), n = (uint32_t)(e - b);
+      c.seq = std::vector<uint8_t>(c.seq.begin() + (size_t)i0 * c.L, c.seq.begin() + (size_t)(i0 + n) * c.L);
+      c.names = std::vector<std::string>(c.names.begin() + i0, c.names.begin() + i0 + n);
+      c.nseq = n;
+      q.global_base += i0;
+      kept.push_back(std::move(q));
+    }
+    at = chunk_end;
+  }
+  queries_.swap(kept);
+}
+
 // ------------------------------------------------------------------ session
-Session::Session(const AlignerOptions &opt) : opt_(opt) {
+Session::Session(const AlignerOptions &opt, uint32_t shard_rank, uint32_t shard_world) : opt_(opt) {
   threads_ = HostThreads();
   DeviceModule &dev = DeviceModule::Get();
   dev.Bind(opt_.device);
@@ -178,6 +240,8 @@ Session::Session(const AlignerOptions &opt) : opt_(opt) {
     if (!(id <= opt_.end_query_chunk)) break;
   }
   if (queries_.empty()) throw std::runtime_error("[Aligner] error: don't find query file.");
+  if (shard_world == 0 || shard_rank >= shard_world) throw std::invalid_argument("shard rank outside the world");
+  if (shard_world > 1) ApplyShard(shard_rank, shard_world);  // may leave no queries
 
   DbFile df(opt_.db_prefix);
   db_sum_u32_ = (uint32_t)df.sum_length;
@@ -202,12 +266,7 @@ Session::Session(const AlignerOptions &opt) : opt_(opt) {
       q.group_last.push_back(q.group_end[i] - 1);
     }
     q.qlen.assign(n, 1);
-    for (uint32_t i = 0; i < n; ++i) {
-      const uint8_t *s = &q.chunk.seq[(size_t)i * L];
-      uint32_t e = L - 1;
-      while (e > 0 && s[e] == kBaseX) --e;
-      q.qlen[i] = e + 1;
-    }
+    for (uint32_t i = 0; i < n; ++i) q.qlen[i] = QueryLength(&q.chunk.seq[(size_t)i * L], L);
     q.dev = dev.UploadQuery(q.chunk.seq.data(), n, L);
     dev.SetQueryGroups(q.dev, q.group_first.data(), q.group_last.data(), (uint32_t)q.group_first.size());
   }
@@ -374,8 +433,12 @@ void Session::DeviceMergePath(QueryData &q, DbData &d, const std::vector<uint32_
   const uint32_t base = q.chunk.L + 2 * opt_.extend + 2 * (1u << opt_.log_region);
   const uint32_t tb_base = q.chunk.L + 2 * opt_.extend * 2 * (1u << opt_.log_region);
   const uint32_t cap = std::max<uint32_t>(opt_.best, 1);
-  // segments of ~16M candidates (fewer host round trips per step)
-  const uint64_t kSegmentCands = 16ull << 20, kTailCands = 1ull << 20;
+  // segments of ~16M candidates (fewer host round trips per step);
+  // GHOSTM_SEGMENT_CANDS / GHOSTM_TAIL_CANDS shrink them so that small test
+  // datasets run the many-segment pipeline of the full-size workloads
+  uint64_t kSegmentCands = 16ull << 20, kTailCands = 1ull << 20;
+  if (const char *e = getenv("GHOSTM_SEGMENT_CANDS")) kSegmentCands = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
+  if (const char *e = getenv("GHOSTM_TAIL_CANDS")) kTailCands = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
   const uint32_t ng = (uint32_t)q.group_first.size();
   auto group_begin = [&](uint32_t g) { return offsets[q.group_first[g]]; };
   // segment cuts (group ranges) first, so each segment's K2 tasks can be built
@@ -418,6 +481,7 @@ void Session::DeviceMergePath(QueryData &q, DbData &d, const std::vector<uint32_
     stats_.seconds_merge += NowSeconds() - t0;
     for (uint32_t c : *sel_counts) stats_.tracebacks += c;
     if (c1 > c0) dev.AppendRecords(q.dev, g0, *sel_counts, cap, q.global_base, d.global_base);
+    stats_.segments += 1;
     Part *part = NewPart();
     const QueryData *qp = &q;
     formatter_->Submit([this, qp, g0, sel_counts, sel_hits, cap, part] {
@@ -724,6 +788,8 @@ void Session::Run() {
   stats_.merge_launches = dt.merge_launches;
   stats_.merge_launches_wave = dt.merge_launches_wave;
   stats_.score_launches_framed = dt.score_launches_framed;
+  for (int c = 0; c < 4; ++c) stats_.seed_queries_class[c] = dt.seed_queries_class[c];
+  stats_.seed_queries_wide = dt.seed_queries_wide;
   for (size_t k = 0; k < used_parts_; ++k)
     for (const auto &h : parts_[k].hits) stats_.hits += h.size();
 }

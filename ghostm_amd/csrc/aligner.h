@@ -90,9 +90,20 @@ class TaskQueue {
   std::thread worker_;
 };
 
+// Multi-GPU shards: cuts[0..world] splitting n queries into
+// contiguous ranges of about equal total weight, cut only where group_start[i]
+// is set (a name group's first query); ghostm_amd/shard.py balanced_cuts is the
+// same rule.
+void ShardCuts(uint64_t n, const uint32_t *weight, const uint8_t *group_start, uint32_t world, uint64_t *cuts);
+
 class Session {
  public:
-  explicit Session(const AlignerOptions &opt);
+  // shard_rank/shard_world: search only that shard of the query set (one
+  // process per GPU); the shards' outputs concatenated in rank order are the
+  // unsharded output, and hit records keep global query indices.
+  explicit Session(const AlignerOptions &opt, uint32_t shard_rank = 0, uint32_t shard_world = 1);
+  uint64_t ShardBegin() const { return shard_begin_; }
+  uint64_t ShardEnd() const { return shard_end_; }
   ~Session();
 
   void Run();                          // whole search; replaces previous results
@@ -128,6 +139,7 @@ class Session {
   };
   using Results = std::vector<std::vector<HitRecord>>;
 
+  void ApplyShard(uint32_t rank, uint32_t world);
   void RunQueryChunk(QueryData &q);
   void DeviceMergePath(QueryData &q, DbData &d, const std::vector<uint32_t> &counts,
                        const std::vector<uint64_t> &offsets, uint64_t total);
@@ -141,6 +153,7 @@ class Session {
   const LineFormat &Format();
 
   AlignerOptions opt_;
+  uint64_t shard_begin_ = 0, shard_end_ = UINT64_MAX;  // query range over the loaded chunks
   std::vector<QueryData> queries_;
   std::vector<DbData> dbs_;
   uint32_t db_sum_u32_ = 0;           // DBReader::GetSumDbLength() truncates to u32

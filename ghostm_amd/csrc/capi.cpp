@@ -26,6 +26,37 @@ void *GhostmSessionCreate(int argc, char **argv) {
   }
 }
 
+void *GhostmSessionCreateShard(int argc, char **argv, int rank, int world) {
+  try {
+    if (world < 1 || rank < 0 || rank >= world) throw Error("shard rank outside 0..world-1");
+    AlignerOptions opt = ParseAlignerOptions(argc, argv);
+    return new Session(opt, (uint32_t)rank, (uint32_t)world);
+  } catch (std::exception &e) {
+    SetLastErrorMessage(e.what());
+    return nullptr;
+  }
+}
+
+int GhostmSessionShardRange(void *s, uint64_t *begin, uint64_t *end) {
+  if (!s) return 1;
+  const Session *p = static_cast<Session *>(s);
+  if (begin) *begin = p->ShardBegin();
+  if (end) *end = p->ShardEnd();
+  return 0;
+}
+
+int GhostmShardCuts(uint64_t n, const uint32_t weights[], const uint8_t group_start[], int world,
+                    uint64_t cuts[]) {
+  try {
+    if (world < 1) throw Error("world must be >= 1");
+    ShardCuts(n, weights, group_start, (uint32_t)world, cuts);
+    return 0;
+  } catch (std::exception &e) {
+    SetLastErrorMessage(e.what());
+    return 1;
+  }
+}
+
 int GhostmSessionRun(void *s) {
   try {
     if (!s) throw Error("null session");

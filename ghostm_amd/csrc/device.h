@@ -55,6 +55,8 @@ struct DeviceTimes {
   uint64_t traceback_launches_scan = 0, traceback_scan_cells = 0;  // K3a scores-only pass
   uint64_t score_launches_framed = 0;  // f16 K2 launches of the column-framed kernel (k_score16f)
   uint64_t merge_launches = 0, merge_launches_wave = 0;            // K4 (k_merge_wave: one wave per group)
+  uint64_t seed_queries_class[4] = {0, 0, 0, 0};  // K1 queries per size class (3 = global merge)
+  uint64_t seed_queries_wide = 0;                 // ... redone by the offset pass (more than a slot)
 };
 
 class DeviceModule {

@@ -164,6 +164,14 @@ void DeviceModule::Bind(int device) {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 16384 * 4));
   HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_seed<512, 8192, false>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 8192 * 4));
+  HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_seed<256, 4096, false>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 4096 * 4));
+  HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_seed_hash<256, 8192>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 8192 * 4));
+  HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_seed_hash<512, 12288>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 12288 * 4));
+  HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_seed_hash<1024, 24576>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 24576 * 4));
   const int scan_lds = (int)kScanLds;
 #define GHOSTM_SCAN_ATTR(SS, HH, EE, FF)                                             \
   HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_tb_scan<SS, HH, EE, FF>,       \
@@ -323,6 +331,31 @@ struct SeedClass {
 };
 static const SeedClass kSeedClasses[] = {{256, 4096}, {512, 8192}, {1024, 16384}, {1024, 0}};
 
+// Test knobs (read per Seed call): GHOSTM_K1_CAPS="c0,c1,c2" lowers the three
+// LDS class caps (never raises them: every kernel keeps its LDS sizing), so
+// small datasets reach every class and the global-merge class 3;
+// GHOSTM_K1_SLOT_CAP lowers the per-query slot, sending more queries through
+// the offset pass that rewrites wide queries in place.
+static void SeedCaps(uint32_t caps[3], uint32_t *slot_cap) {
+  for (int k = 0; k < 3; ++k) caps[k] = kSeedClasses[k].cap;
+  if (const char *e = getenv("GHOSTM_K1_CAPS")) {
+    const char *p = e;
+    for (int k = 0; k < 3 && *p; ++k) {
+      char *end = nullptr;
+      const unsigned long v = strtoul(p, &end, 10);
+      if (end == p) break;
+      caps[k] = std::min<uint32_t>(caps[k], (uint32_t)v);
+      p = *end == ',' ? end + 1 : end;
+    }
+    for (int k = 1; k < 3; ++k) caps[k] = std::max(caps[k], caps[k - 1]);
+  }
+  *slot_cap = kSlotCap;
+  if (const char *e = getenv("GHOSTM_K1_SLOT_CAP")) {
+    const unsigned long v = strtoul(e, nullptr, 10);
+    if (v >= 1) *slot_cap = std::min<uint32_t>(kSlotCap, (uint32_t)v);
+  }
+}
+
 template <uint32_t B, uint32_t C, bool G>
 static void LaunchSeed(const kern::SeedArgs &a, uint32_t items, hipStream_t s) {
   const size_t lds = G ? 0 : (size_t)2 * C * 4;
@@ -372,9 +405,11 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
   if (nlists > kern::kMaxLists) throw Error("too many seed lists");
   if (d->kcl == 0) throw Error("database index missing");
 
+  uint32_t caps[3], slot_cap;
+  SeedCaps(caps, &slot_cap);
   I.counts.Reserve((size_t)nq * 4);
   I.nelem.Reserve((size_t)nq * 4);
-  I.slots.Reserve((size_t)nq * kSlotCap * 4);
+  I.slots.Reserve((size_t)nq * slot_cap * 4);
   I.offsets.Reserve((size_t)nq * 8);
   I.list_beg.Reserve((size_t)nq * nlists * 4);
   I.list_len.Reserve((size_t)nq * nlists * 4);
@@ -411,7 +446,7 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
     if (n == 0) continue;
     int c = 3;
     for (int k = 0; k < 3; ++k)
-      if (n <= kSeedClasses[k].cap) { c = k; break; }
+      if (n <= caps[k]) { c = k; break; }
     cls[c].push_back(i);
     if (c == 3) {
       goff.push_back(gtotal);
@@ -442,7 +477,7 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
   a.list_len = I.list_len.as<uint32_t>();
   a.counts = I.counts.as<uint32_t>();
   a.slots = I.slots.as<uint32_t>();
-  a.slot_cap = kSlotCap;
+  a.slot_cap = slot_cap;
   a.gbuf = I.gbuf.as<uint32_t>();
   a.gbuf_off = I.gbuf_off.as<unsigned long long>();
   // K1b pass 1: every class, candidates into per-query slots (largest first).
@@ -475,7 +510,7 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
   for (int c = 0; c < 4; ++c) {
     size_t gi = 0;
     for (uint32_t qi : cls[c]) {
-      if ((*counts)[qi] > kSlotCap) {
+      if ((*counts)[qi] > slot_cap) {
         wide[c].push_back(qi);
         if (c == 3) wide_goff.push_back(goff[gi]);
       }
@@ -488,13 +523,15 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
   HIP_CHECK(hipMemcpyAsync(I.offsets.p, offsets->data(), (size_t)nq * 8, hipMemcpyHostToDevice, S(stream_)));
   // slot -> compact
   hipLaunchKernelGGL(kern::k_compact, dim3((nq + 3) / 4), dim3(256), 0, S(stream_),
-                     I.slots.as<uint32_t>(), kSlotCap, I.counts.as<uint32_t>(), (const uint8_t *)nullptr,
+                     I.slots.as<uint32_t>(), slot_cap, I.counts.as<uint32_t>(), (const uint8_t *)nullptr,
                      I.offsets.as<unsigned long long>(), nq, I.cand_start.as<uint32_t>(),
                      I.cand_qid.as<uint32_t>());
   HIP_CHECK(hipGetLastError());
   // pass 2: queries with more candidates than a slot, written straight into place
   size_t nwide = 0;
   for (auto &v : wide) nwide += v.size();
+  for (int c = 0; c < 4; ++c) times_.seed_queries_class[c] += cls[c].size();
+  times_.seed_queries_wide += nwide;
   std::vector<uint32_t> all;  // outlives the async copy
   if (nwide) {
     all.reserve(nwide);

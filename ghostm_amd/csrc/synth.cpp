@@ -9,6 +9,9 @@
 //   DNA reads (-t dna): length -l nt; a fraction `homolog` back-translate a random
 //     subject segment (random synonymous codons, `subst` of them mutated), the rest
 //     are uniform random bases.
+//   -D FASTA: queries sample the subjects of an existing FASTA instead (the
+//     BASELINE config-2 substitute: testset/db.fasta, whose large_queries.fasta is
+//     absent from the reference); substrings are clipped to the subject length.
 // RNG: splitmix64, so the files are identical on every host.
 #include <getopt.h>
 
@@ -89,9 +92,10 @@ int SynthMain(int argc, char **argv) {
   double homolog = 0.8, subst = 0.15;
   bool dna = false;
   uint32_t read_len = 150;
+  std::string subjects_from;
   optind = 1;
   int c;
-  while ((c = getopt(argc, argv, "d:q:n:N:s:a:b:m:x:h:u:p:f:t:l:")) >= 0) {
+  while ((c = getopt(argc, argv, "d:q:n:N:s:a:b:m:x:h:u:p:f:t:l:D:")) >= 0) {
     switch (c) {
       case 'd': db_path = optarg; break;
       case 'q': q_path = optarg; break;
@@ -108,6 +112,7 @@ int SynthMain(int argc, char **argv) {
       case 'f': first = strtoull(optarg, nullptr, 10); break;
       case 't': dna = strcmp(optarg, "dna") == 0; break;
       case 'l': read_len = atoi(optarg); break;
+      case 'D': subjects_from = optarg; break;
       default: throw std::invalid_argument("synth: bad option");
     }
   }
@@ -118,6 +123,24 @@ int SynthMain(int argc, char **argv) {
   SplitMix64 rdb(seed * 1000003ull + 17);
   std::vector<std::string> subjects;
   uint64_t total = 0;
+  if (!subjects_from.empty()) {
+    FILE *f = fopen(subjects_from.c_str(), "r");
+    if (!f) throw std::runtime_error("synth: cannot read " + subjects_from);
+    char line[4096];
+    while (fgets(line, sizeof(line), f)) {
+      if (line[0] == '>') {
+        subjects.emplace_back();
+        continue;
+      }
+      if (subjects.empty()) continue;
+      for (const char *p = line; *p; ++p)
+        if ((*p >= 'A' && *p <= 'Z') || (*p >= 'a' && *p <= 'z') || *p == '*') subjects.back().push_back(*p);
+    }
+    fclose(f);
+    while (!subjects.empty() && subjects.back().empty()) subjects.pop_back();
+    if (subjects.empty()) throw std::runtime_error("synth: no subjects in " + subjects_from);
+    db_res = 0;  // no generated subjects
+  }
   while (total < db_res) {
     const uint32_t len = rdb.Range(smin, smax);
     std::string s(len, 'A');

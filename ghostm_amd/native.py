@@ -65,10 +65,21 @@ class GhostmStats(ctypes.Structure):
         ("merge_launches", c_uint64),
         ("merge_launches_wave", c_uint64),
         ("score_launches_framed", c_uint64),
+        ("seed_queries_class", c_uint64 * 4),
+        ("seed_queries_wide", c_uint64),
+        ("segments", c_uint64),
     ]
 
     def as_dict(self) -> dict:
-        return {name: getattr(self, name) for name, _ in self._fields_}
+        out = {}
+        for name, _ in self._fields_:
+            v = getattr(self, name)
+            if name == "seed_queries_class":
+                for k in range(4):
+                    out[f"seed_queries_class{k}"] = v[k]
+            else:
+                out[name] = v
+        return out
 
 
 # name -> (restype, argtypes); covers every function declared in the header
@@ -90,6 +101,9 @@ SIGNATURES = {
     "GhostmBuildIndexGpu": (c_int, [POINTER(ctypes.c_uint8), c_uint32, c_uint32, c_uint32, u32p, u32p, u32p, c_int,
                                     POINTER(c_float)]),
     "GhostmSessionCreate": (c_void_p, [c_int, POINTER(c_char_p)]),
+    "GhostmSessionCreateShard": (c_void_p, [c_int, POINTER(c_char_p), c_int, c_int]),
+    "GhostmSessionShardRange": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
+    "GhostmShardCuts": (c_int, [c_uint64, u32p, POINTER(ctypes.c_uint8), c_int, POINTER(c_uint64)]),
     "GhostmSessionRun": (c_int, [c_void_p]),
     "GhostmSessionOutput": (c_size_t, [c_void_p, c_char_p, c_size_t]),
     "GhostmSessionWrite": (c_int, [c_void_p]),

@@ -27,15 +27,17 @@ def balanced_cuts(weights: Sequence[int], names: Sequence[str], world: int) -> l
         raise ValueError("world must be >= 1")
     # group starts: a query starts a group unless its name equals the previous one
     starts = [i for i in range(n) if i == 0 or names[i] != names[i - 1]]
-    prefix = np.concatenate([[0], np.cumsum(np.asarray(weights, dtype=np.int64))])
-    total = int(prefix[-1])
+    prefix = [0]
+    for w in weights:
+        prefix.append(prefix[-1] + int(w))
+    total = prefix[-1]
     cuts = [0]
     for r in range(1, world):
-        target = total * r / world
-        # first group start whose prefix weight reaches the target
+        # first group start at or after the previous cut whose prefix weight
+        # reaches total * r / world (integer comparison, as GhostmShardCuts)
         best = n
         for s in starts:
-            if s >= cuts[-1] and prefix[s] >= target:
+            if s >= cuts[-1] and prefix[s] * world >= total * r:
                 best = s
                 break
         cuts.append(max(cuts[-1], best))
@@ -88,3 +90,32 @@ def gather_hits(hits: np.ndarray, dist, device) -> list[np.ndarray] | None:
     if rank != 0:
         return None
     return [g[: int(s.item())].cpu().numpy().view(hits.dtype) for g, s in zip(gathered, sizes)]
+
+
+def gather_bytes(data: bytes, dist, device="cpu") -> list[bytes] | None:
+    """Gather every rank's byte string (e.g. its formatted output) to rank 0 in
+    rank order; None on other ranks."""
+    import torch
+
+    payload = torch.frombuffer(bytearray(data), dtype=torch.uint8) if data else torch.zeros(0, dtype=torch.uint8)
+    parts = gather_device_records(payload.to(device), dist, 1)
+    if parts is None:
+        return None
+    return [p.cpu().numpy().tobytes() for p in parts]
+
+
+def shard_cuts_native(weights, group_start, world: int) -> list[int]:
+    """GhostmShardCuts (the C ABI the shard sessions use), for tests."""
+    import ctypes
+
+    from . import native
+
+    w = np.ascontiguousarray(weights, dtype=np.uint32)
+    g = np.ascontiguousarray(group_start, dtype=np.uint8)
+    cuts = np.zeros(world + 1, dtype=np.uint64)
+    rc = native.load().GhostmShardCuts(len(w), w.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                                       g.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), world,
+                                       cuts.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)))
+    if rc != 0:
+        raise ValueError(native.last_error())
+    return [int(x) for x in cuts]

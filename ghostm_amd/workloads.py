@@ -1,0 +1,72 @@
+"""BASELINE.json workloads as deterministic recipes.
+
+Each recipe names the `ghostm synth` arguments of its query set (every query is a
+function of (seed, index), so `-f first -n count` writes exactly a range of the
+full set), its DB (generated, or an existing FASTA) and the `qry`/`aln` options.
+bench.py builds its inputs from these, tests/golden/make_full_golden.py pins the
+reference CPU program's full output for each, and the GPU tests rebuild them to
+compare with that pin.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(PKG)
+GHOSTM = os.path.join(PKG, "bin", "ghostm")
+GOLDEN = os.path.join(REPO, "tests", "golden")
+TESTSET_DB = os.path.join(GOLDEN, "testset_db.fasta")
+PAM250 = os.path.join(GOLDEN, "matrices", "PAM250")
+
+WORKLOADS = {
+    # configs[1] substitute: testset/large_queries.fasta is absent from the reference
+    # (.MISSING_LARGE_BLOBS); 100k queries of 20-127 aa sampled from the
+    # testset/db.fasta subjects (80 %, 15 % substitutions) or background-random,
+    # searched against testset/db.fasta
+    "cfg2": {"synth": ["-s", "2", "-a", "20", "-b", "127", "-D", TESTSET_DB], "queries": 100_000,
+             "db": ("fasta", TESTSET_DB), "qry": ["-l", "127"], "aln": [],
+             "workload": "cfg2 substitute: 100k queries (20-127 aa) sampled from testset/db.fasta subjects "
+                         "vs testset/db.fasta"},
+    "cfg3": {"synth": ["-s", "3", "-N", "5000000"], "queries": 100_000, "db": ("synth", 5_000_000, 3),
+             "qry": ["-l", "300"], "aln": [],
+             "workload": "cfg3: synthetic 100k queries (L=127) x 5M-residue DB"},
+    "cfg4": {"synth": ["-s", "4", "-N", "10000000"], "queries": 1_000_000, "db": ("synth", 10_000_000, 4),
+             "qry": ["-l", "300"], "aln": [],
+             "workload": "cfg4: synthetic 1M queries (avg 300 aa requested, L=127) x 10M-residue DB"},
+    "cfg5": {"synth": ["-s", "5", "-N", "5000000"], "queries": 100_000, "db": ("synth", 5_000_000, 5),
+             "qry": ["-l", "300"], "aln": ["-r", "64", "-M", PAM250, "-y", "2"],
+             "workload": "cfg5: wide band -r 64, PAM250 11/1, -y 2; synthetic 100k queries x 5M-residue DB"},
+}
+
+
+def _run(exe: str, *args: str) -> None:
+    subprocess.run([exe, *args], check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+
+
+def make_db(name: str, root: str, exe: str = GHOSTM) -> str:
+    """Format the workload's DB under root (formatter `exe`: this repo's `ghostm`,
+    or the reference program for the golden pins). Returns the DB prefix."""
+    w = WORKLOADS[name]
+    os.makedirs(root, exist_ok=True)
+    prefix = os.path.join(root, "db")
+    if w["db"][0] == "synth":
+        _, residues, seed = w["db"]
+        _run(GHOSTM, "synth", "-d", f"{root}/db.fa", "-N", str(residues), "-s", str(seed))
+        _run(exe, "db", "-i", f"{root}/db.fa", "-o", prefix)
+        os.remove(f"{root}/db.fa")
+    else:
+        _run(exe, "db", "-i", w["db"][1], "-o", prefix)
+    return prefix
+
+
+def make_queries(name: str, root: str, first: int = 0, count: int | None = None, exe: str = GHOSTM) -> str:
+    """Format queries [first, first + count) of the workload under root; returns
+    the query prefix."""
+    w = WORKLOADS[name]
+    n = w["queries"] - first if count is None else count
+    os.makedirs(root, exist_ok=True)
+    _run(GHOSTM, "synth", "-q", f"{root}/q.fa", "-n", str(n), "-f", str(first), *w["synth"])
+    _run(exe, "qry", "-i", f"{root}/q.fa", "-o", f"{root}/q", *w["qry"])
+    os.remove(f"{root}/q.fa")
+    return f"{root}/q"

@@ -158,6 +158,9 @@ typedef struct GhostmStats {
   uint64_t merge_launches;          /* K4 launches */
   uint64_t merge_launches_wave;     /* ... that ran one wave per name group (k_merge_wave) */
   uint64_t score_launches_framed;   /* f16 K2 launches of the column-framed kernel (k_score16f) */
+  uint64_t seed_queries_class[4];   /* K1 queries per size class by list entries (3 = global merge) */
+  uint64_t seed_queries_wide;       /* K1 queries with more candidates than a slot (offset pass) */
+  uint64_t segments;                /* device-merge segments (K2 -> K4 -> K3 rounds) */
 } GhostmStats;
 
 /* Session: parse `aln` options exactly like the reference (getopt string
@@ -165,6 +168,29 @@ typedef struct GhostmStats {
  * load every query and DB chunk and make them resident on the device given by
  * -D (default 0). Returns NULL on error. */
 void *GhostmSessionCreate(int argc, char **argv);
+
+/* Multi-GPU (the reference has no multi-GPU path, common.h:37):
+ * one process per GPU, each opening a shard session. The query set selected by
+ * -i/-S/-L is cut into `world` contiguous ranges of about equal residues, only
+ * at name-group starts (a DNA read's six frames stay together: the reference
+ * merges a group into one result list, aligner.cpp:697-700), and this session
+ * searches range `rank` on the device given by -D. Hit records keep global
+ * query indices, and the shards' outputs concatenated in rank order are the
+ * unsharded output byte for byte; the single collective is the caller's gather
+ * of GhostmSessionDeviceHits records (RCCL over xGMI). Returns NULL on error.
+ * world = 1 is GhostmSessionCreate. */
+void *GhostmSessionCreateShard(int argc, char **argv, int rank, int world);
+
+/* The query range [begin, end) of a shard session, as indices over the
+ * selected chunks' queries (0, UINT64_MAX for an unsharded session). */
+int GhostmSessionShardRange(void *session, uint64_t *begin, uint64_t *end);
+
+/* The shard rule on its own (host only, no device): cuts[0..world] over n
+ * queries of the given weights; a cut falls only where group_start[i] != 0 and
+ * is the first such i at or after the previous cut with
+ * sum(weights[0..i)) * world >= sum(weights) * r. */
+int GhostmShardCuts(uint64_t n, const uint32_t weights[], const uint8_t group_start[], int world,
+                    uint64_t cuts[]);
 
 /* Run the whole search with the CPU path's semantics (batch cuts, merge order,
  * tie rules) on the device. Results replace those of any previous run. */

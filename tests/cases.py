@@ -54,7 +54,79 @@ DATASETS = {
         ("db", ["-i", "{d}/db.fa", "-o", "{d}/db", "-l", "1"]),
         ("qry", ["-i", "{d}/q.fa", "-o", "{d}/q", "-l", "300", "-L", "1"]),
     ],
+    # the cfg4 generator's own DB (10M residues, seed 4) and its first 5000
+    # queries: the K1 size classes of the headline workload (97 % class 1,
+    # 3 % class 2), its candidate density and the >256-candidate pass
+    "syn_scale": [
+        ("synth", ["-d", "{d}/db.fa", "-q", "{d}/q.fa", "-n", "5000", "-N", "10000000", "-s", "4"]),
+        ("db", ["-i", "{d}/db.fa", "-o", "{d}/db"]),
+        ("qry", ["-i", "{d}/q.fa", "-o", "{d}/q", "-l", "300"]),
+    ],
+    # low-complexity subjects and queries (poly-Q, AKE repeats): K1 class 3
+    # (global merge, > 16384 list entries), queries with ~1000 candidates (the
+    # offset pass) and name groups of heavily tied scores beyond the K4 wave
+    # kernel's LDS capacity (its one-lane fallback), std::sort ties decide subjects
+    "syn_repeat": [
+        ("synth", ["-d", "{d}/db.fa", "-q", "{d}/q.fa", "-n", "300", "-N", "200000", "-s", "13"]),
+        ("py", ["gen_repeat", "{d}"]),
+        ("db", ["-i", "{d}/db.fa", "-o", "{d}/db"]),
+        ("qry", ["-i", "{d}/q.fa", "-o", "{d}/q", "-l", "300"]),
+    ],
+    # BASELINE configs[1] substitute at 20 % scale (the full 100k set is pinned in
+    # full_golden.json): queries of 20-127 aa sampled from testset/db.fasta
+    "cfg2_20k": [
+        ("synth", ["-q", "{d}/q.fa", "-n", "20000", "-s", "2", "-a", "20", "-b", "127", "-D",
+                   "{golden}/testset_db.fasta"]),
+        ("db", ["-i", "{golden}/testset_db.fasta", "-o", "{d}/db"]),
+        ("qry", ["-i", "{d}/q.fa", "-o", "{d}/q", "-l", "127"]),
+    ],
+    # the same queries against a one-subject DB (DB::GetID's early return,
+    # reference db.h:115-117, is the only branch taken)
+    "cfg2_single": [
+        ("synth", ["-q", "{d}/q.fa", "-n", "5000", "-s", "2", "-a", "20", "-b", "127", "-D",
+                   "{golden}/testset_db.fasta"]),
+        ("py", ["gen_single_subject", "{golden}/testset_db.fasta", "{d}/db.fa"]),
+        ("db", ["-i", "{d}/db.fa", "-o", "{d}/db"]),
+        ("qry", ["-i", "{d}/q.fa", "-o", "{d}/q", "-l", "127"]),
+    ],
 }
+
+
+def gen_repeat(d: str) -> None:
+    """Append deterministic low-complexity subjects and queries to a synth
+    dataset (syn_repeat)."""
+    import random
+
+    r = random.Random(1313)
+    aa = "ARNDCQEGHILKMFPSTWYV"
+
+    def mutate(s: str, rate: float) -> str:
+        return "".join(aa[r.randrange(20)] if r.random() < rate else ch for ch in s)
+
+    def fasta(name: str, seq: str) -> str:
+        return f">{name}\n" + "".join(seq[i:i + 60] + "\n" for i in range(0, len(seq), 60))
+
+    with open(f"{d}/db.fa", "a") as f:
+        for i in range(40):
+            f.write(fasta(f"polyQ{i}", mutate("Q" * r.randint(300, 600), 0.03)))
+        for i in range(20):
+            f.write(fasta(f"ake{i}", mutate("AKE" * r.randint(100, 200), 0.03)))
+    with open(f"{d}/q.fa", "a") as f:
+        for i in range(4):
+            f.write(fasta(f"rq{i}", mutate("Q" * r.randint(127, 200), 0.02 * i)))
+        for i in range(4):
+            f.write(fasta(f"rake{i}", mutate("AKE" * r.randint(43, 70), 0.02 * i)))
+        for i in range(6):  # a low-complexity island inside a random query
+            left = "".join(r.choice(aa) for _ in range(r.randint(10, 60)))
+            right = "".join(r.choice(aa) for _ in range(r.randint(10, 60)))
+            f.write(fasta(f"rmix{i}", left + ("Q" if i % 2 else "AKE") * r.randint(4, 12) + right))
+
+
+def gen_single_subject(src: str, out: str) -> None:
+    """The first record of a FASTA file (cfg2_single's one-subject DB)."""
+    recs = open(src).read().split(">")[1:]
+    with open(out, "w") as f:
+        f.write(">" + recs[0])
 
 # (dataset, variant name, aln option list, env)
 VARIANTS = [
@@ -88,7 +160,22 @@ VARIANTS = [
     ("syn_chunks", "default", [], {}),
     ("syn_chunks", "S1", ["-S", "1"], {}),
     ("syn_chunks", "L0", ["-L", "0"], {}),
+    ("syn_scale", "default", [], {}),
+    ("syn_repeat", "default", [], {}),
+    ("syn_repeat", "b20_y2", ["-b", "20", "-y", "2"], {}),
+    ("cfg2_20k", "default", [], {}),
+    ("cfg2_20k", "y2", ["-y", "2"], {}),
+    ("cfg2_single", "default", [], {}),
+] + [
+    # BASELINE configs[4]: -r 64, PAM250, -y 2 over the whole gap sweep
+    # {8,10,11,14} x {1,2} (G11/E1 is syn_small/r64_pam250 above)
+    ("syn_small", f"r64_pam250_g{g}e{e}", ["-r", "64", "-M", PAM250, "-G", str(g), "-E", str(e), "-y", "2"], {})
+    for g in (8, 10, 11, 14) for e in (1, 2) if (g, e) != (11, 1)
 ]
+
+# variants whose oracle run takes more than a few seconds: GPU tests only (their
+# golden values come from the reference program itself)
+SLOW_FOR_ORACLE = {"syn_chunks", "syn_scale", "cfg2_20k"}
 
 # batch-cut cases (-l in candidates via the test hook); oracle-checked only
 BATCH_VARIANTS = [
@@ -117,7 +204,10 @@ def build_dataset(name: str, root: str) -> str:
     os.makedirs(d, exist_ok=True)
     for tool, args in DATASETS[name]:
         a = [x.format(d=d, golden=GOLDEN) for x in args]
-        subprocess.run([GHOSTM, tool] + a, check=True, capture_output=True)
+        if tool == "py":
+            globals()[a[0]](*a[1:])
+        else:
+            subprocess.run([GHOSTM, tool] + a, check=True, capture_output=True)
     open(stamp, "w").close()
     return d
 
@@ -162,3 +252,33 @@ def parse_ncbi_matrix(path: str):
                 m[code(r) * 32 + code(head[i - 1])] = int(v)
         n += 1
     return m
+
+
+def k1_list_entries(d: str, qprefix: str = "q", dprefix: str = "db", shift: int = 2) -> "np.ndarray":
+    """Per query of chunk 0: the number of K1 list entries (positions p >= j*shift
+    over the query's seed lists j), which picks the K1 size class
+    (ghostm_amd/csrc/device.hip SeedCaps). Numpy restatement of the list
+    selection of SearchNextCpu (reference aligner.cpp:399-430), for the tests
+    that assert every class runs."""
+    import numpy as np
+
+    inf = np.fromfile(f"{d}/{qprefix}_0.inf", dtype="<u4")
+    nq, L = int(inf[0]), int(inf[1])
+    q = np.fromfile(f"{d}/{qprefix}_0.seq", dtype=np.uint8)[: nq * L].reshape(nq, L).astype(np.int64)
+    raw = np.fromfile(f"{d}/{dprefix}_0.ind", dtype="<u4")
+    seed, kcl, npos = (int(x) for x in raw[:3])
+    kc = raw[3:3 + kcl].astype(np.int64)
+    pos = raw[3 + kcl:3 + kcl + npos].astype(np.int64)
+    offs = [t for t in range(32) if (seed >> t) & 1]
+    span = max(offs) + 1
+    nl = (L - span) // shift + 1
+    out = np.zeros(nq, dtype=np.int64)
+    for j in range(nl):
+        key = np.zeros(nq, dtype=np.int64)
+        for t in offs:
+            key = (key << 5) | q[:, j * shift + t]
+        b, e = kc[key], kc[key + 1]
+        # positions before the list's diagonal origin j*shift are skipped
+        lo = np.array([bb + np.searchsorted(pos[bb:ee], j * shift) if ee > bb else bb for bb, ee in zip(b, e)])
+        out += e - lo
+    return out

@@ -1,0 +1,151 @@
+"""GPU parity at the scale the headline workload runs:
+
+* every K1 size class (the LDS hash kernels of classes 0-2 and the global
+  merge of class 3) and the >slot offset pass, shown to run by the session's
+  per-class counters, against the reference golden;
+* the device-merge pipeline cut into many segments with a shrinking tail (the
+  path every cfg3/cfg4 run takes), on small datasets and on the cfg4 generator's
+  own DB;
+* the FULL BASELINE workloads (cfg2 substitute, cfg3, cfg4, cfg5), whose complete
+  output is compared with the sha256 of the reference CPU program's output
+  (tests/golden/full_golden.json, tests/golden/make_full_golden.py).
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import cases
+from ghostm_amd import workloads
+from ghostm_amd.aligner import Session
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(d, opts, env, qprefix="q", dprefix="db"):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        with Session(["-i", os.path.join(d, qprefix), "-d", os.path.join(d, dprefix), "-o", os.path.join(d, "x"),
+                      "-D", "0"] + list(opts)) as s:
+            s.run()
+            text, st, hits = s.output(), s.stats(), s.hits()
+            dev = s.device_hits().cpu().numpy()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    return text, st, hits, dev
+
+
+def _sha(b: bytes) -> str:
+    return hashlib.sha256(b).hexdigest()
+
+
+def _caps(d):
+    """Class caps at the quartiles of the dataset's K1 list-entry counts, so that
+    each of the four classes receives about a quarter of the queries."""
+    n = cases.k1_list_entries(d)
+    q = [int(np.percentile(n[n > 0], p)) for p in (25, 50, 75)]
+    return ",".join(str(x) for x in q)
+
+
+@pytest.mark.parametrize("k1", ["hash", "merge"])
+@pytest.mark.parametrize("ds,var,opts", [("syn_small", "default", []), ("syn_dna", "default", []),
+                                         ("syn_short", "default", []), ("syn_chunks", "default", []),
+                                         ("syn_small", "r4", ["-r", "4"])])
+def test_every_k1_class_and_the_offset_pass(k1, ds, var, opts, dataset, golden):
+    """GHOSTM_K1_CAPS lowers the class caps to the dataset's quartiles and
+    GHOSTM_K1_SLOT_CAP shrinks the slot to 8 candidates: all four classes and the
+    offset pass for wide queries run, in the hash (default) and merge K1 forms."""
+    d = dataset(ds)
+    env = {"GHOSTM_K1_CAPS": _caps(d), "GHOSTM_K1_SLOT_CAP": "8"}
+    if k1 == "merge":
+        env["GHOSTM_K1"] = "merge"
+    text, st, hits, dev = _run(d, opts, env)
+    assert _sha(text) == golden["aln"][f"{ds}/{var}"]["sha256"]
+    for c in range(4):
+        assert st[f"seed_queries_class{c}"] > 0, (c, st)
+    assert st["seed_queries_wide"] > 0
+    assert (st["seed_runs_hash"] == 0) if k1 == "merge" else (st["seed_runs_hash"] > 0)
+    assert dev.tobytes() == hits.tobytes()
+
+
+def test_syn_scale_runs_the_cfg4_classes(dataset, golden):
+    """The cfg4 generator's DB with its first 5000 queries, default options: K1
+    classes 1 and 2 (k_seed_hash<512,12288>, <1024,24576>) and the offset pass
+    run without any knob, and the output is the reference's."""
+    d = dataset("syn_scale")
+    text, st, hits, dev = _run(d, [], {})
+    assert _sha(text) == golden["aln"]["syn_scale/default"]["sha256"]
+    assert st["seed_queries_class1"] > 0 and st["seed_queries_class2"] > 0
+    assert st["seed_queries_wide"] > 0
+    assert st["seed_runs_hash"] > 0
+    assert dev.tobytes() == hits.tobytes()
+
+
+@pytest.mark.parametrize("ds,var,opts", [("syn_repeat", "default", []), ("syn_repeat", "b20_y2", ["-b", "20", "-y", "2"])])
+def test_low_complexity_reaches_class3(ds, var, opts, dataset, golden):
+    """Poly-Q / AKE-repeat queries have > 16384 K1 list entries (class 3, the
+    global merge) and ~1000 candidates each, with tied scores: no knob needed."""
+    d = dataset(ds)
+    text, st, hits, dev = _run(d, opts, {})
+    assert _sha(text) == golden["aln"][f"{ds}/{var}"]["sha256"]
+    assert st["seed_queries_class3"] > 0 and st["seed_queries_wide"] > 0
+    assert dev.tobytes() == hits.tobytes()
+
+
+@pytest.mark.parametrize("ds,var,opts,seg,tail", [
+    ("syn_small", "default", [], 300, 40),
+    ("syn_small", "b20_t1", ["-b", "20", "-t", "1", "-y", "2"], 1000, 100),
+    ("syn_dna", "default", [], 200, 30),
+    ("syn_short", "default", [], 500, 50),
+    ("syn_scale", "default", [], 100_000, 20_000),
+    ("syn_repeat", "default", [], 400, 64),
+    ("cfg2_20k", "default", [], 5000, 1000),
+])
+def test_many_segment_device_pipeline(ds, var, opts, seg, tail, dataset, golden):
+    """The device-merge path cut into many segments (GHOSTM_SEGMENT_CANDS) with
+    the 3/5 shrinking tail down to GHOSTM_TAIL_CANDS, the next segment's K2
+    tasks prepared during the current K2, and per-segment device records: same
+    text as the reference, same device records as host records."""
+    d = dataset(ds)
+    text, st, hits, dev = _run(d, opts, {"GHOSTM_SEGMENT_CANDS": str(seg), "GHOSTM_TAIL_CANDS": str(tail)})
+    assert _sha(text) == golden["aln"][f"{ds}/{var}"]["sha256"]
+    assert st["segments"] >= 4, st["segments"]
+    assert dev.tobytes() == hits.tobytes()
+
+
+# ----------------------------------------------------------- full workloads
+FULL = os.path.join(cases.GOLDEN, "full_golden.json")
+
+
+def _full_pins():
+    if not os.path.exists(FULL):
+        return {}
+    with open(FULL) as f:
+        return {k: v for k, v in json.load(f).items() if isinstance(v, dict)}
+
+
+@pytest.mark.parametrize("name", ["cfg2", "cfg3", "cfg5", "cfg4"])
+def test_full_workload_matches_reference(name, tmp_path):
+    """The complete BASELINE workload, formatted here and searched by the HIP
+    path, against the reference CPU program's full output (sha256, lines)."""
+    pin = _full_pins().get(name)
+    if pin is None:
+        pytest.skip(f"{name} not pinned in full_golden.json")
+    db = workloads.make_db(name, str(tmp_path / "db"))
+    q = workloads.make_queries(name, str(tmp_path / "q"))
+    aln = workloads.WORKLOADS[name]["aln"]
+    with Session(["-i", q, "-d", db, "-o", str(tmp_path / "out"), "-D", "0"] + aln) as s:
+        s.run()
+        text = s.output()
+        st = s.stats()
+    assert len(text) == pin["bytes"]
+    assert text.count(b"\n") == pin["lines"]
+    assert _sha(text) == pin["sha256"]
+    assert st["queries"] == pin["queries"]

@@ -28,6 +28,26 @@ def test_balanced_cuts_never_split_a_name_group():
     assert cuts == [0, 25, 50, 75, 100]
 
 
+def test_native_shard_cuts_equal_python_rule(built):
+    """GhostmShardCuts (used by the shard sessions, C ABI, host only) cuts exactly
+    where balanced_cuts does, on random weights and name-group structures."""
+    from ghostm_amd.shard import shard_cuts_native
+
+    rng = np.random.default_rng(5)
+    for trial in range(300):
+        n = int(rng.integers(0, 60))
+        weights = rng.integers(1, 128, size=n)
+        names, g = [], 0
+        for i in range(n):
+            if i == 0 or rng.random() < 0.6:
+                g += 1
+            names.append(str(g))
+        starts = [1 if i == 0 or names[i] != names[i - 1] else 0 for i in range(n)]
+        for world in (1, 2, 3, 7, 8, 70):
+            assert shard_cuts_native(weights, starts, world) == balanced_cuts(list(weights), names, world), \
+                (trial, world)
+
+
 def _free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

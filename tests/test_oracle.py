@@ -7,7 +7,7 @@ import pytest
 
 import cases
 
-SMALL = [v for v in cases.VARIANTS if v[0] != "syn_chunks"]
+SMALL = [v for v in cases.VARIANTS if v[0] not in cases.SLOW_FOR_ORACLE]
 
 
 def test_readme_known_answer_matches_readme_table(dataset, tmp_path):
