@@ -1,20 +1,33 @@
 """Benchmark of the `aln` hot path (BASELINE.json metric: query residues aligned/s,
-bit-identical hits). Workload = BASELINE.json configs[3] on one GPU per rank:
-synthetic 1M queries (avg ~265 aa before the 127-residue cap, L = 127) against a
-10M-residue DB, default `aln` options (BLOSUM62 11/1, -b 10, -r 16, -t 2, -s 2).
+bit-identical hits). Workload = BASELINE.json configs[3] (cfg4): synthetic 1M
+queries (avg ~265 aa before the 127-residue cap, L = 127) against a 10M-residue
+DB, default `aln` options (BLOSUM62 11/1, -b 10, -r 16, -t 2, -s 2).
 
-    python bench.py [--gpus N --steps K --warmup W] [--queries 1000000]
-                    [--db-residues 10000000] [--cpu-sample 2000] [--no-cpu]
+    python bench.py [--gpus N --steps K --warmup W] [--preset cfg4|cfg3|cfg5|cfg2]
+                    [--queries N] [--cpu-sample 10000] [--cpu-sample-all 16000] [--no-cpu]
 
-A step = one full `aln` pass over the rank's query set with inputs resident in HBM:
-K1 seed -> K2 score -> host merge -> K3 traceback -> E-values + text formatting
-(in memory) -> (N > 1) RCCL gather of the 32-byte hit records to rank 0.
-Multi-GPU: one process per GPU (torchrun); each rank searches its own 1M-query
-shard (weak scaling), hit records are gathered to rank 0 over RCCL.
+A step = one full `aln` pass over the rank's query shard with inputs resident in
+HBM: K1 seed -> K2 score -> K4 merge -> K3 traceback -> E-values + text
+formatting (in memory) -> (N > 1) the one RCCL gather of the 32-byte hit records
+to rank 0.
+
+Multi-GPU (north_star: "shard the query batch across the 8 GPUs ... single RCCL
+gather"): one process per GPU (torchrun). ONE query set is cut into N balanced,
+name-group-aligned shards (GhostmSessionCreateShard); each rank searches its
+shard against a full DB replica, so total work is fixed as N grows ("strong").
+After the timed steps every rank writes its text at its offset of one output
+file, and rank 0 checks the assembled file against the reference pin.
+
+Parity in the line: `full_output_matches_reference` compares the sha256 of the
+whole output of the last timed step (N = 1) or of the assembled file (N > 1) with
+the reference CPU program's output for the same full workload
+(tests/golden/full_golden.json). A mismatch (or a CPU-sample mismatch) nulls
+`value` and exits non-zero.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import shutil
@@ -26,123 +39,107 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
+from ghostm_amd import workloads  # noqa: E402
+
 PEAK_VALU_TOPS = 78.6   # 256 CU x 4 SIMD x 32 lanes/cycle x 2.4 GHz int32 ops (MI355X_MICROARCH.md)
-PEAK_VALU_PK16_TOPS = 157.3  # the same issue rate, two 16-bit ops per lane (v_pk_*_u16/i16)
+PEAK_VALU_PK16_TOPS = 157.3  # the same issue rate, two 16-bit ops per lane (v_pk_*)
 PEAK_HBM_GBS = 8000.0   # HBM3E spec
 SCORE_OPS_PER_CELL = 10  # Gotoh cell: add, max3 (H), add (open), add+max (E), add+max (F), max (colmax)
-
-
-PAM250 = os.path.join(REPO, "tests", "golden", "matrices", "PAM250")
-# BASELINE.json configs: synthetic data, splitmix64 seeds 3/4/5
-PRESETS = {
-    "cfg4": {"queries": 1_000_000, "db": 10_000_000, "seed": 4, "aln": [],
-             "workload": "cfg4: synthetic 1M queries (avg 300 aa requested, L=127) x 10M-residue DB, per rank"},
-    "cfg3": {"queries": 100_000, "db": 5_000_000, "seed": 3, "aln": [],
-             "workload": "cfg3: synthetic 100k queries (L=127) x 5M-residue DB, per rank"},
-    "cfg5": {"queries": 100_000, "db": 5_000_000, "seed": 5, "aln": ["-r", "64", "-M", PAM250, "-y", "2"],
-             "workload": "cfg5: wide band -r 64, PAM250 11/1, -y 2; synthetic 100k queries x 5M-residue DB"},
-}
+TB_OPS_PER_CELL = 20     # traceback cell with match/length bookkeeping
+FULL_GOLDEN = os.path.join(REPO, "tests", "golden", "full_golden.json")
+VALU_ISSUE = os.path.join(REPO, "profiles", "r2_valu_issue.json")
+PMC = os.path.join(REPO, "profiles", "pmc_traffic.json")
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_data(root: str, nq: int, db_res: int, first: int, seed: int = 4) -> None:
-    ghostm = os.path.join(REPO, "ghostm_amd", "bin", "ghostm")
-    os.makedirs(root, exist_ok=True)
-    run = lambda *a: subprocess.run([ghostm, *a], check=True, stdout=subprocess.DEVNULL,  # noqa: E731
-                                    stderr=subprocess.DEVNULL)
-    run("synth", "-d", f"{root}/db.fa", "-q", f"{root}/q.fa", "-n", str(nq), "-N", str(db_res),
-        "-s", str(seed), "-f", str(first))
-    run("db", "-i", f"{root}/db.fa", "-o", f"{root}/db")
-    run("qry", "-i", f"{root}/q.fa", "-o", f"{root}/q", "-l", "300")
-    os.remove(f"{root}/q.fa")
+def make_data(root: str, preset: str, nq: int) -> tuple[str, str]:
+    db = workloads.make_db(preset, os.path.join(root, "db"))
+    q = workloads.make_queries(preset, os.path.join(root, "q"), 0, nq)
+    return q, db
 
 
-def cpu_baseline(root: str, nsample: int, db_res: int, first: int, seed: int = 4,
-                 aln_args: list | None = None) -> dict:
-    """The reference's own CPU path (oracle/_ref/ghostm_ref: GHOSTM's aligner.cpp
-    compiled from the reference sources, run without -D) on the first `nsample`
-    queries of this rank's workload against the same DB, single-threaded as the
-    reference is. Falls back to this repo's CPU restatement (oracle/ghostm_oracle)
-    when the reference build is absent. Also checks that the GPU output on that
-    sample is byte-identical to the CPU program's."""
-    ghostm = os.path.join(REPO, "ghostm_amd", "bin", "ghostm")
+def _exe():
     ref = os.path.join(REPO, "oracle", "_ref", "ghostm_ref")
     port = os.path.join(REPO, "oracle", "_build", "ghostm_oracle")
-    use_ref = os.path.exists(ref)
-    exe = ref if use_ref else port
-    sub = os.path.join(root, "sample")
-    os.makedirs(sub, exist_ok=True)
-    subprocess.run([ghostm, "synth", "-q", f"{sub}/q.fa", "-n", str(nsample), "-N", str(db_res),
-                    "-s", str(seed), "-f", str(first)], check=True, capture_output=True)
-    subprocess.run([ghostm, "qry", "-i", f"{sub}/q.fa", "-o", f"{sub}/q", "-l", "300"], check=True,
-                   capture_output=True)
-    t0 = time.perf_counter()
-    subprocess.run([exe, "aln", "-i", f"{sub}/q", "-d", f"{root}/db", "-o", f"{sub}/cpu.out"]
-                   + list(aln_args or []), check=True, capture_output=True)
-    dt = time.perf_counter() - t0
+    return (ref, "reference") if os.path.exists(ref) else (port, "port")
+
+
+def _gpu_text(q: str, db: str, aln: list) -> tuple[bytes, int]:
     from ghostm_amd.aligner import Session
 
-    with Session(["-i", f"{sub}/q", "-d", f"{root}/db", "-o", f"{sub}/gpu.out", "-D", str(_device())]
-                 + list(aln_args or [])) as s:
+    with Session(["-i", q, "-d", db, "-o", os.devnull, "-D", str(_device())] + aln) as s:
         s.run()
-        gpu = s.output()
-        residues = s.stats()["query_residues"]
-    same = gpu == open(f"{sub}/cpu.out", "rb").read()
-    what = ("reference aligner.cpp CPU path (oracle/_ref/ghostm_ref, reference sources, g++ -O2)" if use_ref
-            else "CPU restatement (oracle/ghostm_oracle.cpp, g++ -O2)")
-    return {"value": residues / dt, "unit": "query residues/s", "cores": 1,
-            "kind": "reference" if use_ref else "port",
-            "sample": f"first {nsample} queries of rank 0's workload vs the same {db_res / 1e6:g}M-residue DB "
-                      f"({residues} residues, {dt:.1f} s, {what}, 1 thread)",
-            "bit_identical_to_gpu_on_sample": bool(same), "residues": residues}
+        return s.output(), s.stats()["query_residues"]
 
 
-def cpu_baseline_multi(root: str, nsample: int, db_res: int, first: int, residues: int, seed: int = 4,
-                       aln_args: list | None = None, procs: int | None = None) -> dict | None:
-    """SURVEY §8 d4's second CPU figure: the same sample on all host cores the job
-    may use. The reference aligner is single-threaded, so it runs as `procs`
-    processes over contiguous query ranges (queries are independent; the
-    concatenated outputs must equal the one-process output, checked here)."""
-    ref = os.path.join(REPO, "oracle", "_ref", "ghostm_ref")
-    port = os.path.join(REPO, "oracle", "_build", "ghostm_oracle")
-    exe = ref if os.path.exists(ref) else port
-    ghostm = os.path.join(REPO, "ghostm_amd", "bin", "ghostm")
-    # the box's CPU share is 16 (OMP_NUM_THREADS is set to it); os.cpu_count()
-    # there reports the whole machine
-    procs = procs or max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)),
-                                os.cpu_count() or 1))
-    sub = os.path.join(root, "sample")
-    parts = []
+def cpu_baseline(root: str, preset: str, db: str, nsample: int, aln: list) -> dict:
+    """The reference's own CPU path (oracle/_ref/ghostm_ref: GHOSTM's aligner.cpp
+    compiled from the reference sources, run without -D; this repo's restatement
+    oracle/ghostm_oracle where the reference build is absent) on the first
+    `nsample` queries of the workload, single-threaded as the reference is. The
+    GPU output on the same sample must be byte-identical."""
+    exe, kind = _exe()
+    q = workloads.make_queries(preset, os.path.join(root, "cpu1"), 0, nsample)
+    out = os.path.join(root, "cpu1", "cpu.out")
+    t0 = time.perf_counter()
+    subprocess.run([exe, "aln", "-i", q, "-d", db, "-o", out] + aln, check=True, capture_output=True)
+    dt = time.perf_counter() - t0
+    gpu, residues = _gpu_text(q, db, aln)
+    same = gpu == open(out, "rb").read()
+    what = ("reference aligner.cpp CPU path (oracle/_ref/ghostm_ref, reference sources, g++ -O2)"
+            if kind == "reference" else "CPU restatement (oracle/ghostm_oracle.cpp, g++ -O2)")
+    return {"value": residues / dt, "unit": "query residues/s", "cores": 1, "kind": kind,
+            "sample": f"first {nsample} queries of the workload vs the same DB ({residues} residues, "
+                      f"{dt:.1f} s incl. the process's file loads, {what}, 1 thread)",
+            "bit_identical_to_gpu_on_sample": bool(same)}
+
+
+def reference_split(root: str, preset: str, db: str, nsample: int, aln: list, procs: int):
+    """The CPU program (reference build, else the restatement) over the first
+    `nsample` queries as `procs` concurrent processes on contiguous query ranges.
+    Returns (concatenated output, wall seconds, processes, queries per process),
+    or None if a process failed."""
+    exe, _ = _exe()
     per = (nsample + procs - 1) // procs
+    parts = []
     for k in range(procs):
         n = min(per, nsample - k * per)
         if n <= 0:
             break
-        d = os.path.join(sub, f"part{k}")
-        os.makedirs(d, exist_ok=True)
-        subprocess.run([ghostm, "synth", "-q", f"{d}/q.fa", "-n", str(n), "-N", str(db_res), "-s", str(seed),
-                        "-f", str(first + k * per)], check=True, capture_output=True)
-        subprocess.run([ghostm, "qry", "-i", f"{d}/q.fa", "-o", f"{d}/q", "-l", "300"], check=True,
-                       capture_output=True)
-        parts.append(d)
+        d = os.path.join(root, f"part{k}")
+        parts.append((workloads.make_queries(preset, d, k * per, n), d))
     t0 = time.perf_counter()
-    running = [subprocess.Popen([exe, "aln", "-i", f"{d}/q", "-d", f"{root}/db", "-o", f"{d}/cpu.out"]
-                                + list(aln_args or []), stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
-               for d in parts]
+    running = [subprocess.Popen([exe, "aln", "-i", q, "-d", db, "-o", f"{d}/cpu.out"] + aln,
+                                stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL) for q, d in parts]
     rcs = [p.wait() for p in running]
     dt = time.perf_counter() - t0
     if any(rcs):
         return None
-    joined = b"".join(open(f"{d}/cpu.out", "rb").read() for d in parts)
-    single = open(f"{sub}/cpu.out", "rb").read()
-    return {"value": residues / dt, "unit": "query residues/s", "cores": len(parts),
-            "kind": "reference" if exe == ref else "port",
-            "sample": f"the cpu_baseline sample as {len(parts)} processes over contiguous query ranges "
-                      f"({dt:.1f} s)",
-            "identical_to_one_process": joined == single}
+    return b"".join(open(f"{d}/cpu.out", "rb").read() for _, d in parts), dt, len(parts), per
+
+
+def cpu_baseline_all_cores(root: str, preset: str, db: str, nsample: int, aln: list) -> dict | None:
+    """SURVEY §8 d4's second CPU figure: the reference on all host cores the job
+    may use, as one process per core over contiguous query ranges (the reference
+    is single-threaded; queries are independent). The concatenated outputs must
+    equal the GPU output on the same sample."""
+    exe, kind = _exe()
+    # the box's CPU share is 16 (OMP_NUM_THREADS is set to it); os.cpu_count()
+    # there reports the whole machine
+    procs = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), os.cpu_count() or 1))
+    split = reference_split(os.path.join(root, "cpuN"), preset, db, nsample, aln, procs)
+    if split is None:
+        return None
+    joined, dt, nparts, per = split
+    q = workloads.make_queries(preset, os.path.join(root, "cpuN", "all"), 0, nsample)
+    gpu, residues = _gpu_text(q, db, aln)
+    return {"value": residues / dt, "unit": "query residues/s", "cores": nparts, "kind": kind,
+            "sample": f"first {nsample} queries as {nparts} processes over contiguous query ranges "
+                      f"({per} each, {dt:.1f} s incl. each process's file loads)",
+            "bit_identical_to_gpu_on_sample": joined == gpu}
 
 
 def _device() -> int:
@@ -151,34 +148,42 @@ def _device() -> int:
     return int(os.environ.get("GHOSTM_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0")))
 
 
-def load_pmc_traffic() -> dict | None:
-    p = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if os.path.exists(p):
-        with open(p) as f:
+def _json(path: str) -> dict | None:
+    if os.path.exists(path):
+        with open(path) as f:
             return json.load(f)
     return None
+
+
+def full_pin(preset: str, nq: int, aln: list) -> dict | None:
+    """The reference pin for this exact workload, if it is the full preset."""
+    pins = _json(FULL_GOLDEN) or {}
+    pin = pins.get(preset)
+    w = workloads.WORKLOADS[preset]
+    if not isinstance(pin, dict) or nq != w["queries"] or aln != w["aln"]:
+        return None
+    return pin
 
 
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--preset", choices=sorted(PRESETS), default="cfg4",
+    ap.add_argument("--preset", choices=sorted(workloads.WORKLOADS), default="cfg4",
                     help="BASELINE.json config (cfg4 = the headline workload)")
-    ap.add_argument("--queries", type=int, default=None, help="queries per rank (default: preset)")
-    ap.add_argument("--db-residues", type=int, default=None)
-    ap.add_argument("--cpu-sample", type=int, default=2000)
+    ap.add_argument("--queries", type=int, default=None, help="queries of the whole job (default: preset)")
+    ap.add_argument("--cpu-sample", type=int, default=10000, help="queries of the 1-core CPU baseline")
+    ap.add_argument("--cpu-sample-all", type=int, default=16000, help="queries of the all-cores CPU baseline")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--workdir", default=None)
-    ap.add_argument("--aln", default="", help="extra aln options appended to the preset's (e.g. '-l 64')")
+    ap.add_argument("--aln", default="", help="extra aln options appended to the preset's (e.g. '-l 16')")
     args = ap.parse_args()
-    preset = PRESETS[args.preset]
-    if args.queries is None:
-        args.queries = preset["queries"]
-    if args.db_residues is None:
-        args.db_residues = preset["db"]
-    aln_args = list(preset["aln"]) + args.aln.split()
+    preset = args.preset
+    w = workloads.WORKLOADS[preset]
+    nq = args.queries or w["queries"]
+    aln_args = list(w["aln"]) + args.aln.split()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -193,22 +198,32 @@ def main() -> None:
         backend = os.environ.get("GHOSTM_BENCH_BACKEND", "nccl")
         dist.init_process_group(backend)
         coll_dev = "cuda" if backend == "nccl" else "cpu"
-    from ghostm_amd.aligner import Session
+    from ghostm_amd.aligner import HIT_DTYPE, Session
 
-    workdir = args.workdir or tempfile.mkdtemp(prefix=f"ghostm_bench_r{rank}_")
+    # one data set for the whole job, built by rank 0 (ranks share the host)
+    if args.workdir:
+        workdir = args.workdir
+    elif world > 1:
+        workdir = os.path.join(tempfile.gettempdir(), f"ghostm_bench_{os.environ.get('MASTER_PORT', '0')}")
+    else:
+        workdir = tempfile.mkdtemp(prefix="ghostm_bench_")
     t0 = time.perf_counter()
-    first = rank * args.queries
-    make_data(workdir, args.queries, args.db_residues, first, seed=preset["seed"])
-    log(f"[rank {rank}] data ready in {time.perf_counter() - t0:.1f}s at {workdir}")
-    sess = Session(["-i", f"{workdir}/q", "-d", f"{workdir}/db", "-o", f"{workdir}/out", "-D", str(_device())]
-                   + aln_args)
+    if rank == 0:
+        qprefix, dbprefix = make_data(workdir, preset, nq)
+        log(f"[rank 0] data ready in {time.perf_counter() - t0:.1f}s at {workdir}")
+    if dist is not None:
+        dist.barrier()
+    qprefix, dbprefix = os.path.join(workdir, "q", "q"), os.path.join(workdir, "db", "db")
+    out_path = os.path.join(workdir, "out")
+    argv = ["-i", qprefix, "-d", dbprefix, "-o", out_path, "-D", str(_device())] + aln_args
+    sess = Session(argv, shard=(rank, world) if world > 1 else None)
 
     def step():
         sess.run()
         if dist is not None:
-            from ghostm_amd.aligner import HIT_DTYPE
             from ghostm_amd.shard import gather_device_records
 
+            # the single data-path collective: hit records to rank 0
             merged = gather_device_records(sess.device_hits().to(coll_dev), dist, HIT_DTYPE.itemsize)
             if rank == 0:
                 step.gathered = sum(m.numel() for m in merged) // HIT_DTYPE.itemsize
@@ -248,13 +263,80 @@ def main() -> None:
     else:
         total_res = float(st_acc["query_residues"])
 
+    # ---- parity of the timed workload's whole output (last timed step)
+    pin = full_pin(preset, nq, aln_args)
+    text = sess.output()
+    matches = None
+    if world == 1:
+        if pin:
+            matches = (len(text) == pin["bytes"] and hashlib.sha256(text).hexdigest() == pin["sha256"])
+    else:
+        import torch
+
+        # every rank writes its text at its offset of the one output file
+        n = torch.tensor([len(text)], device=coll_dev, dtype=torch.int64)
+        sizes = [torch.zeros_like(n) for _ in range(world)]
+        dist.all_gather(sizes, n)
+        off = sum(int(s.item()) for s in sizes[:rank])
+        total_bytes = sum(int(s.item()) for s in sizes)
+        if rank == 0:
+            with open(out_path, "wb") as f:
+                f.truncate(total_bytes)
+        dist.barrier()
+        fd = os.open(out_path, os.O_WRONLY)
+        os.pwrite(fd, text, off)
+        os.close(fd)
+        dist.barrier()
+        if rank == 0 and pin:
+            h = hashlib.sha256()
+            with open(out_path, "rb") as f:
+                for blk in iter(lambda: f.read(1 << 24), b""):
+                    h.update(blk)
+            matches = total_bytes == pin["bytes"] and h.hexdigest() == pin["sha256"]
+    del text
+
+    # ---- end to end once: create (file loads + H2D), run, write the output file
+    e2e = None
+    if not args.no_e2e:
+        if dist is not None:
+            dist.barrier()
+        te = time.perf_counter()
+        with Session(argv, shard=(rank, world) if world > 1 else None) as s2:
+            s2.run()
+            if world == 1:
+                s2.write()
+            else:
+                import torch
+
+                t2 = s2.output()
+                n = torch.tensor([len(t2)], device=coll_dev, dtype=torch.int64)
+                sizes = [torch.zeros_like(n) for _ in range(world)]
+                dist.all_gather(sizes, n)
+                fd = os.open(out_path + ".e2e", os.O_WRONLY | os.O_CREAT, 0o644)
+                os.pwrite(fd, t2, sum(int(s.item()) for s in sizes[:rank]))
+                os.close(fd)
+            e2e_res = s2.stats()["query_residues"]
+        dt = time.perf_counter() - te
+        if dist is not None:
+            import torch
+
+            v = torch.tensor([dt, e2e_res], device=coll_dev, dtype=torch.float64)
+            mx = v.clone()
+            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+            dist.all_reduce(v)
+            dt, e2e_res = float(mx[0].item()), float(v[1].item())
+        e2e = {"seconds": dt, "value": e2e_res / dt, "unit": "query residues/s",
+               "includes": "session create (query/DB/index file loads, H2D), the search, text formatting "
+                           "and the output file write (N > 1: every rank writes its slice of the one file)"}
+
     k = args.steps
     per = {key: v / k for key, v in st_acc.items()}
-    cpu = cpu_multi = None
+    cpu = cpu_all = None
     if rank == 0 and world == 1 and not args.no_cpu:  # the CPU baseline is an N=1 figure
-        cpu = cpu_baseline(workdir, args.cpu_sample, args.db_residues, first, preset["seed"], aln_args)
-        cpu_multi = cpu_baseline_multi(workdir, args.cpu_sample, args.db_residues, first,
-                                       cpu.pop("residues"), preset["seed"], aln_args)
+        cpu = cpu_baseline(workdir, preset, dbprefix, min(args.cpu_sample, nq), aln_args)
+        cpu_all = cpu_baseline_all_cores(workdir, preset, dbprefix, min(args.cpu_sample_all, nq), aln_args)
+    ok = matches is not False and all(c is None or c.get("bit_identical_to_gpu_on_sample", True)
+                                      for c in (cpu, cpu_all))
     if rank == 0:
         score_t = per["seconds_score"] / max(1, per["score_launches"])
         score_cells = per["score_cells"] / max(1, per["score_launches"])
@@ -264,85 +346,126 @@ def main() -> None:
         peak = PEAK_VALU_PK16_TOPS if packed else PEAK_VALU_TOPS
         framed = half and per.get("score_launches_framed", 0) == per["score_launches"]
         if framed:
-            kname = ("k_score16f<32> (K2 Gotoh DP, packed f16 holding exact integers in a per-column frame, "
+            kname = ("k_score16f<32> (K2 Gotoh DP, exact integers in packed f16 lanes, per-column frame, "
                      "two candidates per lane)")
         elif half:
-            kname = "k_score16<32,f16> (K2 Gotoh DP, packed f16 holding exact integers, two candidates per lane)"
+            kname = "k_score16<32,f16> (K2 Gotoh DP, exact integers in packed f16 lanes, two candidates per lane)"
         elif packed:
             kname = "k_score16<32,int16> (K2 Gotoh DP, packed int16, two candidates per lane)"
         else:
             kname = "k_score (K2 Gotoh DP, int32)"
-        dtype = "f16" if half else ("int16" if packed else "int32")
-        pmc = load_pmc_traffic()
-        traffic = None
-        if pmc and pmc.get("queries") == args.queries:
-            traffic = pmc.get("k_score_hbm_bytes_per_launch")
+        dtype = ("int (exact integers in packed f16 lanes, int16 re-score above the guard)" if half
+                 else "int16" if packed else "int32")
+        pmc = _json(PMC)
+        pmc_ok = bool(pmc and pmc.get("queries") == nq and world == 1 and preset == "cfg4" and not args.aln)
+        issue = _json(VALU_ISSUE)
+        roof = {
+            "bound": "valu",
+            "kernel": kname,
+            "achieved": achieved,
+            "peak": peak,
+            "unit": "Tops/s",
+            "frac": achieved / peak,
+            "traffic": pmc.get("k_score_hbm_bytes_per_launch") if pmc_ok else None,
+            "cells_per_launch": score_cells,
+            "ops_per_cell": SCORE_OPS_PER_CELL,
+            "gcups": score_cells / score_t / 1e9 if score_t > 0 else 0.0,
+            "avg_launch_ms": score_t * 1e3,
+            "guard_rescores_per_step": per.get("score_rechecks", 0),
+        }
+        if issue and pmc_ok and pmc.get("k_score_valu_insts_per_launch"):
+            # the measured ceiling: chip-wide issue rate of packed/VOP3 instructions
+            # (tools/microbench/valu_issue.hip, profiles/r2_valu_issue.json) against
+            # K2's own VALU instruction count per launch (PMC SQ_INSTS_VALU)
+            rate = pmc["k_score_valu_insts_per_launch"] / score_t
+            roof["valu_insts_per_launch"] = pmc["k_score_valu_insts_per_launch"]
+            roof["issue_rate_ginst_s"] = rate / 1e9
+            roof["measured_issue_peak_ginst_s"] = issue["packed_vop3_ginst_s"]
+            roof["frac_of_measured_issue"] = rate / 1e9 / issue["packed_vop3_ginst_s"]
+        tb_t = per["seconds_traceback"]
+        tb_ach = per["traceback_cells"] * TB_OPS_PER_CELL / tb_t / 1e12 if tb_t > 0 else 0.0
+        roof_k3 = {
+            "bound": "valu",
+            "kernel": "K3 traceback per step (k_tb_scan scores-only reverse scan + k_traceback_key)",
+            "achieved": tb_ach,
+            "peak": PEAK_VALU_TOPS,
+            "unit": "Tops/s",
+            "frac": tb_ach / PEAK_VALU_TOPS,
+            "traceback_cells_per_step": per["traceback_cells"],
+            "scan_cells_per_step": per["traceback_scan_cells"],
+            "ops_per_cell": TB_OPS_PER_CELL,
+            "ms_per_step": tb_t * 1e3,
+        }
         seed_gbs = per["seed_bytes"] / per["seconds_seed"] / 1e9 if per["seconds_seed"] > 0 else 0.0
+        roof_k1 = {
+            "bound": "hbm (nominal; PMC shows the hash kernels issue/latency-bound, see the valu fields)",
+            "kernel": "K1 seed stage per step (k_seed_lists, k_seed_hash, k_compact: gathers of CSR positions)",
+            "achieved": seed_gbs,
+            "peak": PEAK_HBM_GBS,
+            "unit": "GB/s",
+            "frac": seed_gbs / PEAK_HBM_GBS,
+            "algorithmic_bytes_per_step": per["seed_bytes"],
+            "traffic": pmc.get("k1_hbm_bytes_per_step") if pmc_ok else None,
+            "ms_per_step": per["seconds_seed"] * 1e3,
+            "queries_per_class": [per.get(f"seed_queries_class{c}", 0) for c in range(4)],
+        }
+        if issue and pmc_ok and pmc.get("k1_valu_insts_per_step"):
+            rate = pmc["k1_valu_insts_per_step"] / per["seconds_seed"]
+            roof_k1["valu_insts_per_step"] = pmc["k1_valu_insts_per_step"]
+            roof_k1["issue_rate_ginst_s"] = rate / 1e9
+            roof_k1["frac_of_measured_issue"] = rate / 1e9 / issue["packed_vop3_ginst_s"]
         out = {
             "metric": "query residues aligned/sec (whole node) + bit-identical hit-list vs CPU",
-            "value": total_res / elapsed,
+            "value": total_res / elapsed if ok else None,
             "unit": "query residues/s",
             "n_gpus": world,
             "steps": k,
             "warmup": args.warmup,
             "ms_per_step": elapsed / k * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": dtype,
-            "data": f"synthetic (ghostm synth, splitmix64 seed {preset['seed']}; "
-                    f"aln options {' '.join(aln_args) if aln_args else 'defaults (BLOSUM62 11/1)'})",
+            "data": f"synthetic (ghostm synth; {w['workload']}; aln options "
+                    f"{' '.join(os.path.basename(a) for a in aln_args) if aln_args else 'defaults (BLOSUM62 11/1)'})",
             "config": {
-                "workload": preset["workload"],
-                "aln_options": aln_args,
-                "queries_per_rank": args.queries,
-                "db_residues": args.db_residues,
-                "query_residues_per_rank_step": per["query_residues"],
+                "workload": w["workload"] + ("" if nq == w["queries"] else f" (first {nq} queries)"),
+                "aln_options": [os.path.basename(a) for a in aln_args],
+                "queries": nq,
+                "query_residues_per_step": total_res / k,
                 "candidates_per_rank_step": per["candidates"],
                 "hits_per_rank_step": per["hits"],
-                "parallelism": f"query-shard x{world} (one process per GPU, RCCL gather of hit records)",
+                "segments_per_rank_step": per.get("segments", 0),
+                "parallelism": f"query shards x{world} (one process per GPU, balanced, name-group aligned; "
+                               "RCCL gather of hit records to rank 0)",
             },
-            "roofline": {
-                "bound": "valu",
-                "kernel": kname,
-                "achieved": achieved,
-                "peak": peak,
-                "unit": "Tops/s",
-                "frac": achieved / peak,
-                "traffic": traffic,
-                "cells_per_launch": score_cells,
-                "ops_per_cell": SCORE_OPS_PER_CELL,
-                "gcups": score_cells / score_t / 1e9 if score_t > 0 else 0.0,
-                "avg_launch_ms": score_t * 1e3,
-            },
-            "roofline_hbm": {
-                "bound": "hbm",
-                "kernel": "K1 seed stage per step (k_seed_lists, k_seed_hash, k_compact: gathers of CSR positions)",
-                "achieved": seed_gbs,
-                "peak": PEAK_HBM_GBS,
-                "unit": "GB/s",
-                "frac": seed_gbs / PEAK_HBM_GBS,
-                "algorithmic_bytes_per_step": per["seed_bytes"],
-                "traffic": pmc.get("k1_hbm_bytes_per_step") if (pmc and pmc.get("queries") == args.queries) else None,
-            },
+            "full_output_matches_reference": matches,
+            "full_output_reference": (f"sha256 {pin['sha256'][:16]}..., {pin['lines']} lines "
+                                      f"(tests/golden/full_golden.json)") if pin else None,
+            "roofline": roof,
+            "roofline_k1": roof_k1,
+            "roofline_k3": roof_k3,
             "stages_s_per_step": {
                 "total": per["seconds_total"],
                 "seed_device": per["seconds_seed"],
                 "score_device": per["seconds_score"],
                 "traceback_device": per["seconds_traceback"],
-                "merge_host": per["seconds_merge"],
-                "output_host": per["seconds_output"],
+                "merge_select_host_wall": per["seconds_merge"],
+                "output_host_background": per["seconds_output"],
             },
+            "end_to_end": e2e,
             "cpu_baseline": cpu,
-            "cpu_baseline_all_cores": cpu_multi,
+            "cpu_baseline_all_cores": cpu_all,
         }
         print(json.dumps(out), flush=True)
     sess.close()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
-    if not args.workdir:
+    if rank == 0 and not args.workdir:
         shutil.rmtree(workdir, ignore_errors=True)
+    if rank == 0 and not ok:
+        sys.exit(1)
 
 
 if __name__ == "__main__":

@@ -16,23 +16,32 @@ CPU_EXES = [os.path.join(REPO, "oracle", "_ref", "ghostm_ref"), os.path.join(REP
 
 @pytest.mark.skipif(not os.path.exists(GHOSTM) or not any(os.path.exists(p) for p in CPU_EXES),
                     reason="CLI or CPU oracle not built (run __graft_entry__.build())")
-@pytest.mark.parametrize("procs", [1, 3])
-def test_cpu_baseline_all_cores_matches_one_process(tmp_path, procs):
+@pytest.mark.parametrize("preset,procs", [("cfg2", 1), ("cfg2", 3), ("cfg3", 4)])
+def test_cpu_split_matches_one_process(tmp_path, preset, procs):
     import bench
+    from ghostm_amd import workloads
 
     w = str(tmp_path)
-    nq, db_res, first = 60, 200_000, 17
-    bench.make_data(w, nq, db_res, first, seed=3)
-    sub = os.path.join(w, "sample")
-    os.makedirs(sub)
-    subprocess.run([GHOSTM, "synth", "-q", f"{sub}/q.fa", "-n", str(nq), "-N", str(db_res), "-s", "3",
-                    "-f", str(first)], check=True, capture_output=True)
-    subprocess.run([GHOSTM, "qry", "-i", f"{sub}/q.fa", "-o", f"{sub}/q", "-l", "300"], check=True,
-                   capture_output=True)
+    nq = 90
+    db = workloads.make_db(preset, os.path.join(w, "db"))
+    q = workloads.make_queries(preset, os.path.join(w, "one"), 0, nq)
     exe = next(p for p in CPU_EXES if os.path.exists(p))
-    subprocess.run([exe, "aln", "-i", f"{sub}/q", "-d", f"{w}/db", "-o", f"{sub}/cpu.out"], check=True,
-                   capture_output=True)
-    assert os.path.getsize(f"{sub}/cpu.out") > 0
-    r = bench.cpu_baseline_multi(w, nq, db_res, first, residues=1000, seed=3, aln_args=[], procs=procs)
-    assert r is not None and r["cores"] == procs
-    assert r["identical_to_one_process"]
+    aln = workloads.WORKLOADS[preset]["aln"]
+    subprocess.run([exe, "aln", "-i", q, "-d", db, "-o", f"{w}/one.out"] + aln, check=True, capture_output=True)
+    one = open(f"{w}/one.out", "rb").read()
+    assert one
+    joined, dt, nparts, per = bench.reference_split(os.path.join(w, "split"), preset, db, nq, aln, procs)
+    assert nparts == procs and dt > 0
+    assert joined == one
+
+
+def test_full_pin_only_for_the_full_workload():
+    import bench
+    from ghostm_amd import workloads
+
+    pins = bench._json(bench.FULL_GOLDEN) or {}
+    for name, w in workloads.WORKLOADS.items():
+        if name in pins:
+            assert bench.full_pin(name, w["queries"], list(w["aln"])) is not None
+        assert bench.full_pin(name, w["queries"] - 1, list(w["aln"])) is None
+        assert bench.full_pin(name, w["queries"], list(w["aln"]) + ["-b", "3"]) is None

@@ -60,10 +60,10 @@ def _caps(d):
                                          ("syn_small", "r4", ["-r", "4"])])
 def test_every_k1_class_and_the_offset_pass(k1, ds, var, opts, dataset, golden):
     """GHOSTM_K1_CAPS lowers the class caps to the dataset's quartiles and
-    GHOSTM_K1_SLOT_CAP shrinks the slot to 8 candidates: all four classes and the
+    GHOSTM_K1_SLOT_CAP shrinks the slot to 2 candidates: all four classes and the
     offset pass for wide queries run, in the hash (default) and merge K1 forms."""
     d = dataset(ds)
-    env = {"GHOSTM_K1_CAPS": _caps(d), "GHOSTM_K1_SLOT_CAP": "8"}
+    env = {"GHOSTM_K1_CAPS": _caps(d), "GHOSTM_K1_SLOT_CAP": "2"}
     if k1 == "merge":
         env["GHOSTM_K1"] = "merge"
     text, st, hits, dev = _run(d, opts, env)

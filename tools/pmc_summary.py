@@ -75,7 +75,13 @@ def main() -> None:
     fetch, _ = counters(os.path.join(args.prof, "fetch"))
     write, _ = counters(os.path.join(args.prof, "write"))
     sq, sq_dur = counters(os.path.join(args.prof, "sq"))
-    for k in set(fetch) | set(write) | set(sq):
+    lds, _ = counters(os.path.join(args.prof, "lds"))
+    issue = {}
+    ipath = os.path.join(prof, "r2_valu_issue.json")
+    if os.path.exists(ipath):
+        with open(ipath) as f:
+            issue = json.load(f)
+    for k in set(fetch) | set(write) | set(sq) | set(lds):
         e = kernels.setdefault(k, {})
         f = mean(fetch.get(k, {}).get("FETCH_SIZE", {}).values())
         w = mean(write.get(k, {}).get("WRITE_SIZE", {}).values())
@@ -97,8 +103,18 @@ def main() -> None:
             if c.get("SQ_INSTS_VALU") and c.get("GRBM_GUI_ACTIVE"):
                 cyc = c["GRBM_GUI_ACTIVE"] / 8
                 e["valu_issue_util"] = c["SQ_INSTS_VALU"] * 2 / (SIMDS * cyc)
+                e["valu_insts_per_launch"] = c["SQ_INSTS_VALU"]
                 if d:
                     e["effective_clock_ghz"] = cyc / d
+                    # against the measured chip-wide issue rate of packed/VOP3 ops
+                    if issue.get("packed_vop3_ginst_s"):
+                        e["valu_frac_of_measured_issue"] = c["SQ_INSTS_VALU"] / d / issue["packed_vop3_ginst_s"]
+        if k in lds:
+            c = {name: mean(v.values()) for name, v in lds[k].items()}
+            e["lds"] = c
+            if c.get("SQ_LDS_IDX_ACTIVE") and c.get("SQ_LDS_BANK_CONFLICT") is not None:
+                busy = c["SQ_LDS_IDX_ACTIVE"] - c["SQ_LDS_BANK_CONFLICT"]
+                e["lds_bank_conflict_rate"] = c["SQ_LDS_BANK_CONFLICT"] / busy if busy > 0 else None
     with open(os.path.join(prof, f"{args.round}_pmc.json"), "w") as f:
         json.dump({"round": args.round, "queries": args.queries, "kernels": kernels}, f, indent=1, sort_keys=True)
 
@@ -113,10 +129,17 @@ def main() -> None:
     # in the trace / runs in the trace (warmup + steps of the traced command)
     k1 = [k for k in kernels if k.startswith(("k_seed", "k_compact")) and "hbm_bytes_per_launch" in kernels[k]]
     k1_step = sum(kernels[k]["hbm_bytes_per_launch"] * kernels[k].get("launches_in_trace", 0) for k in k1)
+    k1v = [k for k in kernels if k.startswith(("k_seed", "k_compact")) and "valu_insts_per_launch" in kernels[k]]
+    k1v_step = sum(kernels[k]["valu_insts_per_launch"] * kernels[k].get("launches_in_trace", 0) for k in k1v)
+    k2 = [k for k in kernels if k.startswith("k_score") and "valu_insts_per_launch" in kernels[k]]
+    k2_main = max(k2, key=lambda x: kernels[x].get("percent_of_gpu_time", 0)) if k2 else None
     traffic = {"round": args.round, "queries": args.queries,
-               "note": "HBM bytes per launch = FETCH_SIZE*2*1024 + WRITE_SIZE*1024 (gfx950 correction)",
+               "note": "HBM bytes per launch = FETCH_SIZE*2*1024 + WRITE_SIZE*1024 (gfx950 correction); "
+                       "VALU instructions = SQ_INSTS_VALU per dispatch",
                "k_score_hbm_bytes_per_launch": fam("k_score"),
+               "k_score_valu_insts_per_launch": kernels[k2_main]["valu_insts_per_launch"] if k2_main else None,
                "k1_hbm_bytes_per_step": k1_step / args.trace_runs if k1 else None,
+               "k1_valu_insts_per_step": k1v_step / args.trace_runs if k1v else None,
                "k1_kernels": sorted(k1)}
     with open(os.path.join(prof, "pmc_traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1)
