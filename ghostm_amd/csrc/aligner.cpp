@@ -275,6 +275,14 @@ Session::Session(const AlignerOptions &opt, uint32_t shard_rank, uint32_t shard_
     d.dev = dev.UploadDb(c.seq.data(), c.len, c.keys_count.data(), c.kcl, c.positions.data(), c.npos);
     if (c.nseq) dev.SetDbSubjects(d.dev, c.starts.data(), c.nseq);
   }
+  {
+    std::vector<uint32_t> bases;
+    for (const DbData &d : dbs_) bases.push_back(d.global_base);
+    // DB chunk ids are the indices into dbs_ (chunks are read from 0 in order)
+    for (size_t k = 0; k < dbs_.size(); ++k)
+      if (dbs_[k].chunk.id != k) throw Error("DB chunk ids out of order");
+    dev.SetChunkBases(bases.data(), (uint32_t)bases.size());
+  }
   dev.Synchronize();
   formatter_.reset(new TaskQueue());
 }
@@ -418,12 +426,17 @@ void Session::HostMergeBatch(QueryData &q, DbData &d, uint32_t bq0, uint32_t bq1
   }
 }
 
-// Device path: the chunk's groups are cut into segments of ~kSegmentCands
-// candidates (at group boundaries, so every group's candidates stay together as
-// in the single reference batch); per segment K2 -> K4 -> K3 run on the GPU and
-// the segment's text is formatted by the background worker meanwhile.
-void Session::DeviceMergePath(QueryData &q, DbData &d, const std::vector<uint32_t> &counts,
-                              const std::vector<uint64_t> &offsets, uint64_t total) {
+// Device path, one pass per (DB chunk, batch): the chunk's groups are cut into
+// segments of ~kSegmentCands of the batch's candidates (at group boundaries, so
+// every group's candidates stay together as in the reference batch); per
+// segment K2 -> K4 -> K3 run on the GPU. K4 merges each group's candidates with
+// the result list carried from the earlier passes (the reference Merge over
+// result_list, aligner.cpp:687-769, called for every batch of every DB chunk,
+// aligner.cpp:118-174); in the final pass the segment's text is formatted by the
+// background worker while the GPU works on the next one.
+void Session::DevicePass(QueryData &q, DbData &d, const std::vector<uint32_t> &counts,
+                         const std::vector<uint64_t> &offsets, uint32_t bq0, uint32_t bq1, uint64_t c_lo,
+                         uint64_t c_hi, bool carry_in, bool final_pass) {
   DeviceModule &dev = DeviceModule::Get();
   GapConfig gap;
   gap.extend = opt_.extend;
@@ -440,30 +453,59 @@ void Session::DeviceMergePath(QueryData &q, DbData &d, const std::vector<uint32_
   if (const char *e = getenv("GHOSTM_SEGMENT_CANDS")) kSegmentCands = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
   if (const char *e = getenv("GHOSTM_TAIL_CANDS")) kTailCands = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
   const uint32_t ng = (uint32_t)q.group_first.size();
-  auto group_begin = [&](uint32_t g) { return offsets[q.group_first[g]]; };
+  // a group's first candidate of this batch (groups outside it have none)
+  auto group_begin = [&](uint32_t g) { return std::min(std::max(offsets[q.group_first[g]], c_lo), c_hi); };
+  auto group_of = [&](uint32_t qi) {
+    return (uint32_t)(std::upper_bound(q.group_first.begin(), q.group_first.end(), qi) - q.group_first.begin()) - 1;
+  };
+  // the batch's groups [gb0, gb1) (a batch may cut a name group); the groups
+  // before and after it have no new candidates
+  const uint32_t gb0 = bq1 > bq0 ? group_of(bq0) : 0, gb1 = bq1 > bq0 ? group_of(bq1 - 1) + 1 : 0;
   // segment cuts (group ranges) first, so each segment's K2 tasks can be built
   // on the host while the previous segment's K2 runs
   std::vector<std::pair<uint32_t, uint32_t>> cuts;
-  for (uint32_t g0 = 0; g0 < ng;) {
-    const uint64_t rem = total - group_begin(g0);
+  const uint32_t kIdleGroups = 1u << 17;  // groups per segment without candidates
+  auto idle = [&](uint32_t from, uint32_t to) {
+    for (uint32_t g = from; g < to; g += kIdleGroups) cuts.emplace_back(g, std::min(to, g + kIdleGroups));
+  };
+  idle(0, gb0);
+  for (uint32_t g0 = gb0; g0 < gb1;) {
+    const uint64_t rem = c_hi - group_begin(g0);  // candidates from g0 to the batch's end
     // full segments, then shrinking ones (3/5 of what is left, down to
     // kTailCands): each segment's GPU time (~3.5 ms per 1 M candidates) covers
     // the text formatting of the one before it (~1.4 ms per 1 M), so little of
     // the formatting is left when the GPU finishes
-    const uint64_t target = rem > 2 * kSegmentCands ? kSegmentCands : std::max<uint64_t>(kTailCands, rem * 3 / 5);
+    // (a carried pass formats nothing: full segments only)
+    const uint64_t target = rem > 2 * kSegmentCands || !final_pass ? kSegmentCands
+                                                                    : std::max<uint64_t>(kTailCands, rem * 3 / 5);
     uint32_t g1 = g0 + 1;
-    while (g1 < ng && group_begin(g1) - group_begin(g0) < target) ++g1;
+    while (g1 < gb1 && group_begin(g1) - group_begin(g0) < target) ++g1;
     cuts.emplace_back(g0, g1);
     g0 = g1;
   }
+  idle(gb1, ng);
   std::vector<DeviceModule::ScoreSegment> segs;
   for (const auto &c : cuts) {
-    const uint64_t c0 = group_begin(c.first), c1 = c.second < ng ? group_begin(c.second) : total;
+    const uint64_t c0 = group_begin(c.first), c1 = c.second < ng ? group_begin(c.second) : c_hi;
     segs.push_back({c0, c1 - c0, q.group_first[c.first], q.group_last[c.second - 1] + 1});
   }
+  MergePass pass;
+  pass.cand_lo = c_lo;
+  pass.cand_hi = c_hi;
+  pass.carry_in = carry_in;
+  pass.carry_out = !final_pass;
+  pass.chunk = d.chunk.id;
   for (size_t k = 0; k < cuts.size(); ++k) {
     const uint32_t g0 = cuts[k].first, g1 = cuts[k].second;
     const uint64_t c0 = segs[k].cand_begin, c1 = c0 + segs[k].n;
+    // nothing to merge: no candidates and nothing carried (the carry of these
+    // groups is still the empty list ResetCarry left). Groups without new
+    // candidates keep their carried list as it is when -b <= 16: it is sorted
+    // by score, std::sort of <= 16 elements is a stable insertion sort, and
+    // carried entries are all taken (aligner.cpp:719-721); in the final pass
+    // their lists are printed straight from the carry
+    const bool identity = c1 == c0 && carry_in && opt_.best <= 16;
+    const bool work = c1 > c0 || (carry_in && !identity);
     if (c1 > c0) {
       // the next segment's K2 tasks are built while this one's K2 runs
       dev.Score(q.dev, d.dev, c0, c1 - c0, segs[k].q_first, segs[k].q_end, counts, offsets, base, gap, nullptr,
@@ -472,16 +514,18 @@ void Session::DeviceMergePath(QueryData &q, DbData &d, const std::vector<uint32_
     auto sel_counts = std::make_shared<std::vector<uint32_t>>();
     auto sel_hits = std::make_shared<std::vector<SelectedHit>>();
     const double t0 = NowSeconds();
-    if (c1 > c0) {
-      dev.MergeSelect(q.dev, d.dev, g0, g1, c0, c1 - c0, opt_.best, tb_base, opt_.open_gap,
-                      opt_.extend_gap, sel_counts.get(), sel_hits.get());
+    if (work) {
+      dev.MergeSelect(q.dev, d.dev, g0, g1, c0, c1 - c0, opt_.best, tb_base, opt_.open_gap, opt_.extend_gap,
+                      sel_counts.get(), final_pass ? sel_hits.get() : nullptr, pass);
+    } else if (identity && final_pass) {
+      dev.CarryToHost(q.dev, g0, g1, cap, sel_counts.get(), sel_hits.get());
     } else {
       sel_counts->assign(g1 - g0, 0);
     }
     stats_.seconds_merge += NowSeconds() - t0;
-    for (uint32_t c : *sel_counts) stats_.tracebacks += c;
-    if (c1 > c0) dev.AppendRecords(q.dev, g0, *sel_counts, cap, q.global_base, d.global_base);
     stats_.segments += 1;
+    if (!final_pass) continue;
+    if (work || identity) dev.AppendRecords(q.dev, g0, *sel_counts, cap, q.global_base, identity);
     Part *part = NewPart();
     const QueryData *qp = &q;
     formatter_->Submit([this, qp, g0, sel_counts, sel_hits, cap, part] {
@@ -490,10 +534,64 @@ void Session::DeviceMergePath(QueryData &q, DbData &d, const std::vector<uint32_
       stats_.seconds_output += NowSeconds() - t;
     });
   }
-  stats_.batches += 1;
 }
 
 void Session::RunQueryChunk(QueryData &q) {
+  DeviceModule &dev = DeviceModule::Get();
+  SeedConfig sc;
+  sc.threshold = opt_.threshold;
+  sc.shift = opt_.shift;
+  sc.log_region = opt_.log_region;
+  std::vector<uint32_t> counts;
+  std::vector<uint64_t> offsets;
+  // the device merge needs every DB chunk's subject table; GHOSTM_MERGE=host
+  // keeps the host merge (tests)
+  bool device_merge = true;
+  for (const DbData &d : dbs_) device_merge = device_merge && d.chunk.nseq > 0;
+  if (const char *e = getenv("GHOSTM_MERGE")) device_merge = device_merge && strcmp(e, "host") != 0;
+  if (!device_merge) {
+    RunQueryChunkHostMerge(q);
+    return;
+  }
+  const uint32_t cap = std::max<uint32_t>(opt_.best, 1);
+  dev.ResetCarry(q.dev, cap);
+  bool carry = false, formatted = false;
+  for (size_t di = 0; di < dbs_.size(); ++di) {
+    DbData &d = dbs_[di];
+    sc.seed_mask = d.chunk.seed;
+    const uint64_t total = dev.Seed(q.dev, d.dev, sc, &counts, &offsets);
+    stats_.candidates += total;
+    const std::vector<Batch> batches = CpuBatches(counts, opt_.max_list_length);
+    for (size_t bi = 0; bi < batches.size(); ++bi) {
+      const Batch &b = batches[bi];
+      const uint64_t c0 = offsets[b.q0];
+      const uint64_t c1 = b.q1 < counts.size() ? offsets[b.q1] : total;
+      const bool final_pass = di + 1 == dbs_.size() && bi + 1 == batches.size();
+      DevicePass(q, d, counts, offsets, b.q0, b.q1, c0, c1, carry, final_pass);
+      carry = true;
+      formatted = final_pass;
+      stats_.batches += 1;
+    }
+  }
+  if (!formatted) {
+    // the last DB chunk had no batch: the carried lists are the results
+    auto sel_counts = std::make_shared<std::vector<uint32_t>>();
+    auto sel_hits = std::make_shared<std::vector<SelectedHit>>();
+    dev.CarryToHost(q.dev, 0, (uint32_t)q.group_first.size(), cap, sel_counts.get(), sel_hits.get());
+    records_on_device_ = false;  // records are uploaded from the host on demand
+    Part *part = NewPart();
+    const QueryData *qp = &q;
+    formatter_->Submit([this, qp, sel_counts, sel_hits, cap, part] {
+      const double t = NowSeconds();
+      FormatSelected(*qp, 0, *sel_counts, *sel_hits, cap, part);
+      stats_.seconds_output += NowSeconds() - t;
+    });
+  }
+}
+
+// Host merge (GHOSTM_MERGE=host, or a DB chunk without subjects): every batch's
+// scores come back to the host and HostMergeBatch applies the reference Merge.
+void Session::RunQueryChunkHostMerge(QueryData &q) {
   DeviceModule &dev = DeviceModule::Get();
   SeedConfig sc;
   sc.threshold = opt_.threshold;
@@ -508,19 +606,13 @@ void Session::RunQueryChunk(QueryData &q) {
   std::vector<uint32_t> counts;
   std::vector<uint64_t> offsets;
   std::vector<uint32_t> score, end;
-  std::unique_ptr<Results> results;
+  Results results(q.chunk.nseq);
+  records_on_device_ = false;  // host merge: records are uploaded on demand
   for (DbData &d : dbs_) {
     sc.seed_mask = d.chunk.seed;
     const uint64_t total = dev.Seed(q.dev, d.dev, sc, &counts, &offsets);
     stats_.candidates += total;
     const std::vector<Batch> batches = CpuBatches(counts, opt_.max_list_length);
-    if (dbs_.size() == 1 && batches.size() == 1 && batches[0].q0 == 0 &&
-        batches[0].q1 == q.chunk.nseq && d.chunk.nseq > 0) {
-      DeviceMergePath(q, d, counts, offsets, total);
-      return;
-    }
-    if (!results) results.reset(new Results(q.chunk.nseq));
-    records_on_device_ = false;  // host merge: records are uploaded on demand
     for (const Batch &b : batches) {
       const uint64_t c0 = offsets[b.q0];
       const uint64_t c1 = b.q1 < counts.size() ? offsets[b.q1] : total;
@@ -529,15 +621,14 @@ void Session::RunQueryChunk(QueryData &q) {
       end.resize(nc);
       dev.Score(q.dev, d.dev, c0, nc, b.q0, b.q1, counts, offsets, base, gap, score.data(), end.data());
       const double t0 = NowSeconds();
-      HostMergeBatch(q, d, b.q0, b.q1, c0, score.data(), end.data(), counts, offsets, results.get());
+      HostMergeBatch(q, d, b.q0, b.q1, c0, score.data(), end.data(), counts, offsets, &results);
       stats_.seconds_merge += NowSeconds() - t0;
       stats_.batches += 1;
     }
   }
-  if (!results) results.reset(new Results(q.chunk.nseq));
   formatter_->Drain();
   const double t1 = NowSeconds();
-  FormatResults(q, *results, NewPart());
+  FormatResults(q, results, NewPart());
   stats_.seconds_output += NowSeconds() - t1;
 }
 
@@ -720,7 +811,6 @@ void Session::FormatSelected(const QueryData &q, uint32_t g0, const std::vector<
   const unsigned workers = std::max(1u, threads_ > 1 ? threads_ - 1 : 1u);
   out->Reset(workers);
   const LineFormat &w = Format();
-  const DbData &d = dbs_[0];
   ParallelFor(ng, workers, [&](size_t b, size_t e, unsigned t) {
     std::vector<GhostmHit> &ph = out->hits[t];
     size_t nh = 0;
@@ -735,6 +825,7 @@ void Session::FormatSelected(const QueryData &q, uint32_t g0, const std::vector<
       const float scaled = (float)space * w.ev.p.K;
       for (uint32_t k = 0; k < counts[g]; ++k) {
         const SelectedHit &h = hits[(size_t)g * cap + k];
+        const DbData &d = dbs_[h.chunk];
         const uint32_t len = h.ml >> 8, match = h.ml & 0xFFu;
         const float seq_id = (float)match / (float)len;  // aligner.cpp:945
         const std::string &sname = d.chunk.names[h.sid];
@@ -790,6 +881,8 @@ void Session::Run() {
   stats_.score_launches_framed = dt.score_launches_framed;
   for (int c = 0; c < 4; ++c) stats_.seed_queries_class[c] = dt.seed_queries_class[c];
   stats_.seed_queries_wide = dt.seed_queries_wide;
+  stats_.seed_runs_filter = dt.seed_launches_filter;
+  stats_.seed_filter_overflows = dt.seed_filter_overflows;
   for (size_t k = 0; k < used_parts_; ++k)
     for (const auto &h : parts_[k].hits) stats_.hits += h.size();
 }

@@ -141,8 +141,10 @@ class Session {
 
   void ApplyShard(uint32_t rank, uint32_t world);
   void RunQueryChunk(QueryData &q);
-  void DeviceMergePath(QueryData &q, DbData &d, const std::vector<uint32_t> &counts,
-                       const std::vector<uint64_t> &offsets, uint64_t total);
+  void RunQueryChunkHostMerge(QueryData &q);
+  void DevicePass(QueryData &q, DbData &d, const std::vector<uint32_t> &counts,
+                  const std::vector<uint64_t> &offsets, uint32_t bq0, uint32_t bq1, uint64_t c_lo, uint64_t c_hi,
+                  bool carry_in, bool final_pass);
   void HostMergeBatch(QueryData &q, DbData &d, uint32_t bq0, uint32_t bq1, uint64_t cand_begin,
                       const uint32_t *score, const uint32_t *end, const std::vector<uint32_t> &counts,
                       const std::vector<uint64_t> &offsets, Results *results);

@@ -41,7 +41,17 @@ struct DevDb;
 // One hit chosen by the device merge (K4), after its traceback (K3):
 // subject-relative coordinates, ml = (aln_len << 8) | matches.
 struct SelectedHit {
-  uint32_t sid, score, start, end, ml;
+  uint32_t sid, score, start, end, ml, chunk;  // chunk: the hit's DB chunk
+};
+
+// One K4 pass: the batch's candidate range (absolute; a batch may cut a name
+// group) and the carried result lists (reference result_list, aligner.cpp:114):
+// carry_in merges them with the batch's candidates, carry_out keeps the new
+// lists for the next batch or DB chunk.
+struct MergePass {
+  uint64_t cand_lo = 0, cand_hi = UINT64_MAX;
+  bool carry_in = false, carry_out = false;
+  uint32_t chunk = 0;  // DB chunk id of the new hits
 };
 
 struct DeviceTimes {
@@ -57,6 +67,8 @@ struct DeviceTimes {
   uint64_t merge_launches = 0, merge_launches_wave = 0;            // K4 (k_merge_wave: one wave per group)
   uint64_t seed_queries_class[4] = {0, 0, 0, 0};  // K1 queries per size class (3 = global merge)
   uint64_t seed_queries_wide = 0;                 // ... redone by the offset pass (more than a slot)
+  uint64_t seed_launches_filter = 0;              // Seed() calls whose classes 0/1 ran k_seed_filter
+  uint64_t seed_filter_overflows = 0;             // ... queries redone by k_seed_hash (queue overflow)
 };
 
 class DeviceModule {
@@ -64,7 +76,8 @@ class DeviceModule {
   struct Impl;  // device.hip
   static DeviceModule &Get();
 
-  void Bind(int device);                 // hipSetDevice + stream; idempotent
+  void Bind(int device);                 // hipSetDevice + stream; idempotent; one device per process
+  void Use() const;                      // make the bound device current on this thread
   int device() const { return device_; }
   void SetMatrix(const int *m32x32);     // M[db*32 + q]
   std::string DeviceName() const;
@@ -108,17 +121,25 @@ class DeviceModule {
   // empty result lists (first batch, first DB chunk): the reference Merge
   // selection on the device, then the traceback of every selected hit. Uses the
   // scores/ends left on the device by the preceding Score() over the same range.
-  // counts[g] hits per group; hits[g*cap + k], cap = max(best, 1).
+  // counts[g] hits per group; hits[g*cap + k], cap = max(best, 1) (hits may be
+  // null: nothing but the counts is copied back).
   void MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, uint64_t cand_begin, uint64_t n, uint32_t best,
                    uint32_t tb_base, int open, int ext, std::vector<uint32_t> *counts,
+                   std::vector<SelectedHit> *hits, const MergePass &pass = MergePass());
+  // Carried result lists of a query chunk (all groups empty), and their copy to
+  // the host (counts[g], hits[g * cap + k]).
+  void ResetCarry(DevQuery *q, uint32_t cap);
+  void CarryToHost(DevQuery *q, uint32_t g0, uint32_t g1, uint32_t cap, std::vector<uint32_t> *counts,
                    std::vector<SelectedHit> *hits);
+  // Global index of each DB chunk's first subject (hit records' db_id).
+  void SetChunkBases(const uint32_t *bases, uint32_t n);
 
   // Device-resident hit records of the current run (GhostmHit layout, 32 B),
   // for the multi-GPU gather. AppendRecords turns the last MergeSelect's hits
   // (groups [g0, g0 + counts.size())) into records at the end of the array.
   void ResetRecords();
   void AppendRecords(DevQuery *q, uint32_t g0, const std::vector<uint32_t> &counts, uint32_t cap,
-                     uint32_t q_base, uint32_t d_base);
+                     uint32_t q_base, bool from_carry = false);  // from_carry: groups' carried lists
   void UploadRecords(const void *records, uint64_t n);  // host records (other paths)
   uint64_t RecordCount() const { return records_; }
   void CopyRecords(void *dst_device, uint64_t n);         // device-to-device, synchronous

@@ -114,7 +114,10 @@ struct DeviceModule::Impl {
   DevBuf tb_width, tb_ncols, tb_key, tb_order1, tb_order2, tb_sort, tb_pair_a, tb_pair_b, tb_best;
   int cus = 256;
   // K4 work
-  DevBuf keys, sel_count, sel_cand, sel_sid, slot_hits;
+  DevBuf keys, sel_count, sel_cand, sel_sid, slot_hits, sel_from;
+  // result lists carried across batches / DB chunks (per group of the query
+  // chunk: carry_count[g] SlotHits at carry_hits[g * cap]); DB chunk bases
+  DevBuf carry_hits, carry_count, chunk_base;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   DevBuf counters;  // u64 [0] score cells, [1] traceback cells, [2] K3a scan cells
   // K2 tasks of the next segment, built while the current one runs
@@ -139,6 +142,13 @@ struct DeviceModule::Impl {
 };
 
 static constexpr uint32_t kSlotCap = 256;
+// Filtered slot pass (k_seed_filter) of classes 0 and 1, thresholds >= 2:
+// <BLOCK, filter cells, table slots, queue> and its dynamic LDS bytes.
+#define GHOSTM_FILTER0 kern::k_seed_filter<256, 32768, 2304, 1536>
+#define GHOSTM_FILTER1 kern::k_seed_filter<512, 65536, 4608, 3072>
+constexpr size_t kFilterLds0 = (32768 / 16 + 2304 + 1536) * 4;
+constexpr size_t kFilterLds1 = (65536 / 16 + 4608 + 3072) * 4;
+
 // K3a: the pair table (32 x 32 codes x 32 query codes, one word each) + histogram
 static constexpr size_t kScanLds = (size_t)kern::kPairWords * 4 + kern::kSortBins * 4;
 
@@ -147,8 +157,24 @@ DeviceModule &DeviceModule::Get() {
   return *m;
 }
 
+// HIP's current device is per host thread: every entry that allocates or
+// launches makes this module's device current on the calling thread first.
+void DeviceModule::Use() const {
+  thread_local int current = -1;  // this thread's device as last set here
+  if (device_ >= 0 && current != device_) {
+    HIP_CHECK(hipSetDevice(device_));
+    current = device_;
+  }
+}
+
 void DeviceModule::Bind(int device) {
-  if (device_ == device && impl_) return;
+  if (device_ == device && impl_) {
+    Use();
+    return;
+  }
+  // one device per process: buffers, stream and events belong to the first one
+  if (impl_ && device_ >= 0)
+    throw Error("the device module is bound to device " + std::to_string(device_) + "; one device per process");
   int n = 0;
   HIP_CHECK(hipGetDeviceCount(&n));
   if (n <= 0) throw Error("no HIP device visible");
@@ -172,6 +198,10 @@ void DeviceModule::Bind(int device) {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 12288 * 4));
   HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_seed_hash<1024, 24576>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 24576 * 4));
+  HIP_CHECK(hipFuncSetAttribute((const void *)GHOSTM_FILTER0, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)kFilterLds0));
+  HIP_CHECK(hipFuncSetAttribute((const void *)GHOSTM_FILTER1, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)kFilterLds1));
   const int scan_lds = (int)kScanLds;
 #define GHOSTM_SCAN_ATTR(SS, HH, EE, FF)                                             \
   HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_tb_scan<SS, HH, EE, FF>,       \
@@ -207,6 +237,7 @@ size_t DeviceModule::TotalMemory() const {
 }
 
 void DeviceModule::SetMatrix(const int *m) {
+  Use();
   if (!impl_) throw Error("device not bound");
   std::memcpy(impl_->h_matrix, m, sizeof(impl_->h_matrix));
   int k2[32 * 32], tb[32 * 32];
@@ -246,6 +277,7 @@ void DeviceModule::SetMatrix(const int *m) {
 }
 
 DevQuery *DeviceModule::UploadQuery(const uint8_t *seq, uint32_t nseq, uint32_t L) {
+  Use();
   if (!impl_) throw Error("device not bound");
   if (L == 0 || L > kMaxQueryLength)
     throw Error("query record width " + std::to_string(L) + " outside 1..127");
@@ -260,6 +292,7 @@ DevQuery *DeviceModule::UploadQuery(const uint8_t *seq, uint32_t nseq, uint32_t 
 
 DevDb *DeviceModule::UploadDb(const uint8_t *seq, uint32_t len, const uint32_t *kc, uint32_t kcl,
                               const uint32_t *pos, uint32_t npos) {
+  Use();
   if (!impl_) throw Error("device not bound");
   // the kernels index 32-entry tables by residue code
   for (uint32_t k = 0; k < len; ++k)
@@ -279,6 +312,7 @@ DevDb *DeviceModule::UploadDb(const uint8_t *seq, uint32_t len, const uint32_t *
 }
 
 void DeviceModule::Free(DevQuery *q) {
+  if (device_ >= 0) (void)hipSetDevice(device_);  // destructors: never throw
   if (!q) return;
   q->seq.Release();
   q->rcodes.Release();
@@ -288,6 +322,7 @@ void DeviceModule::Free(DevQuery *q) {
 }
 
 void DeviceModule::Free(DevDb *d) {
+  if (device_ >= 0) (void)hipSetDevice(device_);  // destructors: never throw
   if (!d) return;
   d->seq.Release();
   d->kc.Release();
@@ -298,6 +333,7 @@ void DeviceModule::Free(DevDb *d) {
 
 void DeviceModule::SetQueryGroups(DevQuery *q, const uint32_t *first, const uint32_t *last,
                                   uint32_t ng) {
+  Use();
   q->ngroups = ng;
   q->group_first.Reserve((size_t)ng * 4);
   q->group_last.Reserve((size_t)ng * 4);
@@ -308,6 +344,7 @@ void DeviceModule::SetQueryGroups(DevQuery *q, const uint32_t *first, const uint
 }
 
 void DeviceModule::SetDbSubjects(DevDb *d, const uint32_t *starts, uint32_t nsubj) {
+  Use();
   d->nsubj = nsubj;
   d->subj.Reserve((size_t)nsubj * 4);
   if (nsubj) HIP_CHECK(hipMemcpy(d->subj.p, starts, (size_t)nsubj * 4, hipMemcpyHostToDevice));
@@ -362,6 +399,13 @@ static void LaunchSeed(const kern::SeedArgs &a, uint32_t items, hipStream_t s) {
   hipLaunchKernelGGL((kern::k_seed<B, C, G>), dim3(items), dim3(B), lds, s, a);
 }
 
+static void LaunchSeedFilterClass(int cls, const kern::SeedArgs &a, uint32_t items, hipStream_t s) {
+  if (items == 0) return;
+  if (cls == 0) hipLaunchKernelGGL((GHOSTM_FILTER0), dim3(items), dim3(256), kFilterLds0, s, a);
+  else hipLaunchKernelGGL((GHOSTM_FILTER1), dim3(items), dim3(512), kFilterLds1, s, a);
+  HIP_CHECK(hipGetLastError());
+}
+
 // Slot pass of the three LDS classes: the hash-count kernel (table >= 1.5 x cap).
 static void LaunchSeedHashClass(int cls, const kern::SeedArgs &a, uint32_t items, hipStream_t s) {
   if (items == 0) return;
@@ -392,6 +436,7 @@ static void LaunchSeedClass(int cls, const kern::SeedArgs &a, uint32_t items, hi
 
 uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
                             std::vector<uint32_t> *counts, std::vector<uint64_t> *offsets) {
+  Use();
   Impl &I = *impl_;
   const uint32_t nq = q->nseq;
   counts->assign(nq, 0);
@@ -481,24 +526,49 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
   a.gbuf = I.gbuf.as<uint32_t>();
   a.gbuf_off = I.gbuf_off.as<unsigned long long>();
   // K1b pass 1: every class, candidates into per-query slots (largest first).
-  // The LDS classes count bins in a hash table when every bin + 2 < 2^21
-  // (GHOSTM_K1=merge keeps the merge kernel).
+  // The LDS classes count bins in a hash table when every bin + 2 < 2^21;
+  // classes 0 and 1 put the presence filter in front of it when T >= 2
+  // (GHOSTM_K1=merge keeps the merge kernel, =hash the unfiltered table).
   const char *k1 = getenv("GHOSTM_K1");
   const bool hash = !(k1 && strcmp(k1, "merge") == 0) && d->len > 0 &&
                     ((uint64_t)(d->len - 1) >> cfg.log_region) + 2 < kern::kHashBinLimit;
+  const bool filter = hash && cfg.threshold >= 2 && !(k1 && strcmp(k1, "hash") == 0);
   {
     size_t at = list_total;
     for (int c = 3; c >= 0; --c) {
       at -= cls[c].size();
       kern::SeedArgs b = a;
       b.query_list = I.qlist.as<uint32_t>() + at;
-      if (hash && c < 3) LaunchSeedHashClass(c, b, (uint32_t)cls[c].size(), S(stream_));
+      if (filter && c < 2) LaunchSeedFilterClass(c, b, (uint32_t)cls[c].size(), S(stream_));
+      else if (hash && c < 3) LaunchSeedHashClass(c, b, (uint32_t)cls[c].size(), S(stream_));
       else LaunchSeedClass(c, b, (uint32_t)cls[c].size(), S(stream_));
     }
   }
   times_.seed_launches_hash += hash ? 1 : 0;
+  times_.seed_launches_filter += filter ? 1 : 0;
   HIP_CHECK(hipMemcpyAsync(counts->data(), I.counts.p, (size_t)nq * 4, hipMemcpyDeviceToHost, S(stream_)));
   HIP_CHECK(hipStreamSynchronize(S(stream_)));
+  if (filter) {
+    // queries whose filtered queue overflowed: the unfiltered table redoes them
+    std::vector<uint32_t> redo[2];
+    for (int c = 0; c < 2; ++c)
+      for (uint32_t qi : cls[c])
+        if ((*counts)[qi] == kern::kOverflow) redo[c].push_back(qi);
+    if (!redo[0].empty() || !redo[1].empty()) {
+      std::vector<uint32_t> all(redo[0]);
+      all.insert(all.end(), redo[1].begin(), redo[1].end());
+      I.qlist.Reserve(all.size() * 4);
+      HIP_CHECK(hipMemcpyAsync(I.qlist.p, all.data(), all.size() * 4, hipMemcpyHostToDevice, S(stream_)));
+      for (int c = 0; c < 2; ++c) {
+        kern::SeedArgs b = a;
+        b.query_list = I.qlist.as<uint32_t>() + (c ? redo[0].size() : 0);
+        LaunchSeedHashClass(c, b, (uint32_t)redo[c].size(), S(stream_));
+      }
+      HIP_CHECK(hipMemcpyAsync(counts->data(), I.counts.p, (size_t)nq * 4, hipMemcpyDeviceToHost, S(stream_)));
+      HIP_CHECK(hipStreamSynchronize(S(stream_)));
+      times_.seed_filter_overflows += all.size();
+    }
+  }
 
   uint64_t total = 0;
   std::vector<uint32_t> wide[4];
@@ -562,6 +632,7 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
 }
 
 void DeviceModule::CopyStarts(uint64_t begin, uint64_t n, uint32_t *out) {
+  Use();
   if (n == 0) return;
   HIP_CHECK(hipMemcpy(out, impl_->cand_start.as<uint32_t>() + begin, n * 4, hipMemcpyDeviceToHost));
 }
@@ -653,6 +724,7 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
                          uint32_t q_end, const std::vector<uint32_t> &counts,
                          const std::vector<uint64_t> &offsets, uint32_t base,
                          const GapConfig &gap, uint32_t *score, uint32_t *end, const ScoreSegment *next) {
+  Use();
   Impl &I = *impl_;
   if (n == 0) return;
   if (gap.ext > 0) throw Error("positive gap extension score is not supported");
@@ -980,19 +1052,57 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
   times_.traceback_launches_key += key ? 1 : 0;
 }
 
+void DeviceModule::ResetCarry(DevQuery *q, uint32_t cap) {
+  Use();
+  Impl &I = *impl_;
+  const size_t ng = q->ngroups;
+  I.carry_hits.Reserve(ng * cap * sizeof(kern::SlotHit) + 8);
+  I.carry_count.Reserve(ng * 4 + 4);
+  if (ng) HIP_CHECK(hipMemsetAsync(I.carry_count.p, 0, ng * 4, S(stream_)));
+}
+
+void DeviceModule::SetChunkBases(const uint32_t *bases, uint32_t n) {
+  Use();
+  Impl &I = *impl_;
+  I.chunk_base.Reserve((size_t)n * 4 + 4);
+  if (n) HIP_CHECK(hipMemcpy(I.chunk_base.p, bases, (size_t)n * 4, hipMemcpyHostToDevice));
+}
+
+void DeviceModule::CarryToHost(DevQuery *q, uint32_t g0, uint32_t g1, uint32_t cap, std::vector<uint32_t> *counts,
+                               std::vector<SelectedHit> *hits) {
+  Use();
+  Impl &I = *impl_;
+  if (g1 > q->ngroups || g0 > g1) throw Error("group range outside the chunk");
+  const size_t ng = g1 - g0;
+  counts->assign(ng, 0);
+  hits->assign(ng * cap, SelectedHit{});
+  if (ng == 0) return;
+  HIP_CHECK(hipMemcpyAsync(counts->data(), I.carry_count.as<uint32_t>() + g0, ng * 4, hipMemcpyDeviceToHost,
+                           S(stream_)));
+  HIP_CHECK(hipMemcpyAsync(hits->data(), I.carry_hits.as<kern::SlotHit>() + (size_t)g0 * cap,
+                           ng * cap * sizeof(SelectedHit), hipMemcpyDeviceToHost, S(stream_)));
+  HIP_CHECK(hipStreamSynchronize(S(stream_)));
+}
+
 void DeviceModule::MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, uint64_t cand_begin, uint64_t n,
                                uint32_t best, uint32_t tb_base, int open, int ext,
-                               std::vector<uint32_t> *counts, std::vector<SelectedHit> *hits) {
+                               std::vector<uint32_t> *counts, std::vector<SelectedHit> *hits,
+                               const MergePass &pass) {
+  Use();
   Impl &I = *impl_;
   if (g1 > q->ngroups || g0 > g1) throw Error("group range outside the chunk");
   const uint32_t ng = g1 - g0;
   const uint32_t cap = std::max<uint32_t>(best, 1);
   counts->assign(ng, 0);
-  hits->clear();
+  if (hits) hits->clear();
   if (ng == 0) return;
   if (d->nsubj == 0) throw Error("DB subjects not set for the device merge");
   const size_t slots = (size_t)ng * cap;
-  I.keys.Reserve(n * 8 + 8);
+  const bool carry_in = pass.carry_in, carry_out = pass.carry_out;
+  if ((carry_in || carry_out) && I.carry_count.bytes < (size_t)q->ngroups * 4)
+    throw Error("ResetCarry was not called for this query chunk");
+  I.keys.Reserve((n + slots) * 8 + 8);  // per group: its candidates and cap carried keys
+  I.sel_from.Reserve(slots * 4);
   I.sel_count.Reserve((size_t)ng * 4);
   I.sel_cand.Reserve(slots * 4);
   I.sel_sid.Reserve(slots * 4);
@@ -1022,6 +1132,11 @@ void DeviceModule::MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, 
   m.sel_sid = I.sel_sid.as<uint32_t>();
   m.tb_qid = I.tb_qid.as<uint32_t>();
   m.tb_end = I.tb_end.as<uint32_t>();
+  m.cand_lo = pass.cand_lo;
+  m.cand_hi = std::min<uint64_t>(pass.cand_hi, I.ncand);
+  m.carry_count = carry_in ? I.carry_count.as<uint32_t>() + g0 : nullptr;
+  m.carry = carry_in ? I.carry_hits.as<kern::SlotHit>() + (size_t)g0 * cap : nullptr;
+  m.sel_from = carry_in ? I.sel_from.as<uint32_t>() : nullptr;
   hipEvent_t m0 = I.ev0, m1 = I.ev1;
   HIP_CHECK(hipEventRecord(m0, S(stream_)));
   // K4: one wave per name group (keys in LDS) for -b up to kMergeBest, else
@@ -1068,15 +1183,23 @@ void DeviceModule::MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, 
   hipLaunchKernelGGL(kern::k_finalize, dim3((uint32_t)((slots + 255) / 256)), dim3(256), 0, S(stream_),
                      I.sel_count.as<uint32_t>(), I.sel_cand.as<uint32_t>(), I.sel_sid.as<uint32_t>(),
                      I.score_out.as<uint32_t>(), I.end_out.as<uint32_t>(), I.tb_start.as<uint32_t>(),
-                     I.tb_ml.as<uint32_t>(), d->subj.as<uint32_t>(), ng, cap,
-                     I.slot_hits.as<kern::SlotHit>());
+                     I.tb_ml.as<uint32_t>(), d->subj.as<uint32_t>(), ng, cap, pass.chunk,
+                     m.sel_from, m.carry, I.slot_hits.as<kern::SlotHit>());
   HIP_CHECK(hipGetLastError());
   static_assert(sizeof(kern::SlotHit) == sizeof(SelectedHit), "record layout");
-  hits->resize(slots);
+  if (carry_out) {  // the groups' new result lists are the next pass's carry
+    HIP_CHECK(hipMemcpyAsync(I.carry_count.as<uint32_t>() + g0, I.sel_count.p, (size_t)ng * 4,
+                             hipMemcpyDeviceToDevice, S(stream_)));
+    HIP_CHECK(hipMemcpyAsync(I.carry_hits.as<kern::SlotHit>() + (size_t)g0 * cap, I.slot_hits.p,
+                             slots * sizeof(kern::SlotHit), hipMemcpyDeviceToDevice, S(stream_)));
+  }
   unsigned long long cells = 0;
   HIP_CHECK(hipMemcpyAsync(counts->data(), I.sel_count.p, (size_t)ng * 4, hipMemcpyDeviceToHost, S(stream_)));
-  HIP_CHECK(hipMemcpyAsync(hits->data(), I.slot_hits.p, slots * sizeof(SelectedHit), hipMemcpyDeviceToHost,
-                           S(stream_)));
+  if (hits) {  // null: the selection stays on the device (a carried pass)
+    hits->resize(slots);
+    HIP_CHECK(hipMemcpyAsync(hits->data(), I.slot_hits.p, slots * sizeof(SelectedHit), hipMemcpyDeviceToHost,
+                             S(stream_)));
+  }
   unsigned long long scan_cells = 0;
   HIP_CHECK(hipMemcpyAsync(&cells, I.counters.as<unsigned long long>() + 1, 8, hipMemcpyDeviceToHost, S(stream_)));
   HIP_CHECK(hipMemcpyAsync(&scan_cells, I.counters.as<unsigned long long>() + 2, 8, hipMemcpyDeviceToHost,
@@ -1104,7 +1227,8 @@ static void GrowRecords(DevBuf &buf, uint64_t records, uint64_t want, hipStream_
 }
 
 void DeviceModule::AppendRecords(DevQuery *q, uint32_t g0, const std::vector<uint32_t> &counts, uint32_t cap,
-                                 uint32_t q_base, uint32_t d_base) {
+                                 uint32_t q_base, bool from_carry) {
+  Use();
   Impl &I = *impl_;
   const uint32_t ng = (uint32_t)counts.size();
   if (ng == 0) return;
@@ -1119,15 +1243,19 @@ void DeviceModule::AppendRecords(DevQuery *q, uint32_t g0, const std::vector<uin
   GrowRecords(I.records, records_, records_ + total, S(stream_));
   I.rec_prefix.Reserve((size_t)ng * 4);
   HIP_CHECK(hipMemcpyAsync(I.rec_prefix.p, prefix.data(), (size_t)ng * 4, hipMemcpyHostToDevice, S(stream_)));
-  hipLaunchKernelGGL(kern::k_records, dim3((ng + 255) / 256), dim3(256), 0, S(stream_), I.sel_count.as<uint32_t>(),
-                     I.slot_hits.as<kern::SlotHit>(), I.rec_prefix.as<uint32_t>(),
-                     q->group_last.as<uint32_t>() + g0, ng, cap, q_base, d_base,
+  const uint32_t *cnt = from_carry ? I.carry_count.as<uint32_t>() + g0 : I.sel_count.as<uint32_t>();
+  const kern::SlotHit *sh = from_carry ? I.carry_hits.as<kern::SlotHit>() + (size_t)g0 * cap
+                                       : I.slot_hits.as<kern::SlotHit>();
+  hipLaunchKernelGGL(kern::k_records, dim3((ng + 255) / 256), dim3(256), 0, S(stream_), cnt, sh,
+                     I.rec_prefix.as<uint32_t>(),
+                     q->group_last.as<uint32_t>() + g0, ng, cap, q_base, I.chunk_base.as<uint32_t>(),
                      I.records.as<kern::HitRecord32>() + records_);
   HIP_CHECK(hipGetLastError());
   records_ += total;
 }
 
 void DeviceModule::UploadRecords(const void *recs, uint64_t n) {
+  Use();
   Impl &I = *impl_;
   records_ = 0;
   if (n == 0) return;
@@ -1137,6 +1265,7 @@ void DeviceModule::UploadRecords(const void *recs, uint64_t n) {
 }
 
 void DeviceModule::CopyRecords(void *dst, uint64_t n) {
+  Use();
   Impl &I = *impl_;
   n = std::min(n, records_);
   if (n == 0) return;
@@ -1149,6 +1278,7 @@ void DeviceModule::TraceBack(DevQuery *q, DevDb *d, uint32_t n, const uint32_t *
                              const uint32_t *db_end, uint32_t base, int open, int ext,
                              uint32_t *db_start, uint32_t *aln_len, uint32_t *aln_match,
                              float *seq_id) {
+  Use();
   Impl &I = *impl_;
   if (n == 0) return;
   I.tb_qid.Reserve((size_t)n * 4);

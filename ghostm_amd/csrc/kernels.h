@@ -409,6 +409,77 @@ struct BinTable {
   }
 };
 
+// Emission from a filled bin table (k_seed_hash, k_seed_filter): the rule
+// (c(b) > 0 or b = 0) and c(b) + c(b+1) >= T per occupied slot, the count to
+// counts[q], and for queries with <= slot_cap candidates the emitted bins in
+// ascending order into the query's slot.
+template <uint32_t BLOCK, uint32_t TSLOTS>
+__device__ __forceinline__ void EmitFromTable(const SeedArgs &a, uint32_t q, uint32_t *s_tab, uint32_t *s_emit,
+                                              uint32_t *s_part, uint32_t *s_total_p) {
+  constexpr uint32_t kPer = TSLOTS / BLOCK;
+  BinTable<TSLOTS> table{s_tab};
+  const uint32_t tid = threadIdx.x;
+  // 2. emission test per occupied slot (each lane walks only its own occupied
+  //    slots); the phantom bin 0 (c(0) = 0, c(1) >= T)
+  const uint32_t thr = a.threshold;
+  uint32_t mask = 0, mine = 0;
+  bool phantom = false;
+  if (thr != 0) {
+    uint32_t occ = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) occ |= (s_tab[tid + k * BLOCK] != 0 ? 1u : 0u) << k;
+    while (occ) {
+      const uint32_t k = __builtin_ctz(occ);
+      occ &= occ - 1;
+      const uint32_t v = s_tab[tid + k * BLOCK];
+      const uint32_t c = (v >> 3) & 0xFFu;
+      if (c >= thr || c + table.Count(v >> 11) >= thr) {  // bin + 1 = v >> 11
+        mask |= 1u << k;
+        ++mine;
+      }
+    }
+    if (tid == 0 && table.Count(0) == 0 && table.Count(1) >= thr) {
+      phantom = true;
+      ++mine;
+    }
+  }
+  const uint32_t base = BlockExclusiveScan(mine, s_part, s_total_p);
+  const uint32_t total = *s_total_p;
+  if (tid == 0) a.counts[q] = total;
+  if (total == 0 || total > a.slot_cap) return;  // offset pass redoes the wide ones
+
+  // 3. emitted bins -> LDS, rank by value (all distinct), write in order
+  uint32_t at = base;
+  if (phantom) s_emit[at++] = 0;
+  while (mask) {
+    const uint32_t k = __builtin_ctz(mask);
+    mask &= mask - 1;
+    s_emit[at++] = (s_tab[tid + k * BLOCK] >> 11) - 1;
+  }
+  // pad to a multiple of 16 with values above every bin (ranks unaffected)
+  for (uint32_t e = total + tid; e < ((total + 15) & ~15u); e += BLOCK) s_emit[e] = 0xFFFFFFFFu;
+  __syncthreads();
+  // rank of element e = number of smaller ones; four lanes per element, each
+  // counting a quarter of the array with 128-bit reads
+  uint32_t *os = a.slots + (size_t)q * a.slot_cap;
+  const uint32_t n16 = (total + 15) >> 4;  // 16-element blocks
+  for (uint32_t base4 = 0; base4 < total * 4; base4 += BLOCK) {
+    const uint32_t t4 = base4 + tid;
+    const uint32_t e = t4 >> 2, part = t4 & 3;
+    const uint32_t b = e < total ? s_emit[e] : 0u;
+    uint32_t rank = 0;
+    if (e < total) {
+      for (uint32_t blk = 0; blk < n16; ++blk) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(s_emit + blk * 16 + part * 4);
+        rank += (v.x < b) + (v.y < b) + (v.z < b) + (v.w < b);
+      }
+    }
+    rank += __shfl_xor(rank, 1);
+    rank += __shfl_xor(rank, 2);
+    if (e < total && part == 0) os[rank] = b << a.log_region;
+  }
+}
+
 template <uint32_t BLOCK, uint32_t TSLOTS>
 __global__ __launch_bounds__(BLOCK) void k_seed_hash(SeedArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];  // TSLOTS words (dynamic)
@@ -487,65 +558,140 @@ __global__ __launch_bounds__(BLOCK) void k_seed_hash(SeedArgs a) {
   }
   __syncthreads();
 
-  // 2. emission test per occupied slot (each lane walks only its own occupied
-  //    slots); the phantom bin 0 (c(0) = 0, c(1) >= T)
-  const uint32_t thr = a.threshold;
-  uint32_t mask = 0, mine = 0;
-  bool phantom = false;
-  if (thr != 0) {
-    uint32_t occ = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < kPer; ++k) occ |= (s_tab[tid + k * BLOCK] != 0 ? 1u : 0u) << k;
-    while (occ) {
-      const uint32_t k = __builtin_ctz(occ);
-      occ &= occ - 1;
-      const uint32_t v = s_tab[tid + k * BLOCK];
-      const uint32_t c = (v >> 3) & 0xFFu;
-      if (c >= thr || c + table.Count(v >> 11) >= thr) {  // bin + 1 = v >> 11
-        mask |= 1u << k;
-        ++mine;
-      }
-    }
-    if (tid == 0 && table.Count(0) == 0 && table.Count(1) >= thr) {
-      phantom = true;
-      ++mine;
-    }
-  }
-  const uint32_t base = BlockExclusiveScan(mine, s_part, &s_total);
-  const uint32_t total = s_total;
-  if (tid == 0) a.counts[q] = total;
-  if (total == 0 || total > a.slot_cap) return;  // offset pass redoes the wide ones
+  EmitFromTable<BLOCK, TSLOTS>(a, q, s_tab, s_emit, s_part, &s_total);
+}
 
-  // 3. emitted bins -> LDS, rank by value (all distinct), write in order
-  uint32_t at = base;
-  if (phantom) s_emit[at++] = 0;
-  while (mask) {
-    const uint32_t k = __builtin_ctz(mask);
-    mask &= mask - 1;
-    s_emit[at++] = (s_tab[tid + k * BLOCK] >> 11) - 1;
+// K1b'' k_seed_filter<BLOCK, FSLOTS, TSLOTS, QCAP>: k_seed_hash's exact table
+//     behind a presence filter, for thresholds >= 2. Most (list, bin) entries of
+//     a query are lone k-mer hits that can never be emitted: bin b is emitted
+//     only if c(b) + c(b+1) >= T >= 2, so an entry in bin x matters only if
+//     another entry shares x or sits in x + 1 (x is a candidate), or x - 1 is
+//     occupied (x is a candidate's c(b+1)). Pass 1 gathers the entries (kept in
+//     registers, KE per lane) and marks each bin's filter cell, two bits (seen,
+//     seen twice) in an LDS bitmap of FSLOTS cells indexed by the bin's low
+//     bits; aliasing only adds entries. Pass 2 keeps an entry x when x <= 1
+//     (the phantom bin 0 rule reads c(0), c(1)), twice(x), seen(x - 1) or
+//     seen(x + 1), compacted per wave into an LDS queue. Pass 3 counts the
+//     queue in the exact table (TSLOTS >= 1.5 QCAP, so it never fills), and the
+//     emission is k_seed_hash's: every occupied bin and its b + 1 neighbour
+//     have exact counts, so the emitted set and order are identical. A query
+//     whose queue exceeds QCAP is marked kOverflow and redone by k_seed_hash.
+template <uint32_t BLOCK, uint32_t FSLOTS, uint32_t TSLOTS, uint32_t QCAP>
+__global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
+  constexpr uint32_t kFWords = FSLOTS / 16;   // 16 two-bit cells per word
+  uint32_t *const s_flt = s_dyn;
+  uint32_t *const s_tab = s_dyn + kFWords;
+  uint32_t *const s_q = s_tab + TSLOTS;
+  constexpr uint32_t kW = BLOCK / 64;
+  constexpr uint32_t KE = 16;                 // entries per lane: n <= 64 * KE * kW
+  constexpr uint32_t kChunks = KE * kW;
+  constexpr uint32_t kNone = 0xFFFFFFFFu;
+  static_assert((FSLOTS & (FSLOTS - 1)) == 0 && TSLOTS * 2 >= QCAP * 3 && TSLOTS % BLOCK == 0, "filter shape");
+  __shared__ uint32_t s_beg[kMaxLists];
+  __shared__ uint32_t s_off[kMaxLists + 1];
+  __shared__ uint8_t s_cfirst[kChunks];
+  __shared__ __attribute__((aligned(16))) uint32_t s_emit[kMaxSlotCap];
+  __shared__ uint32_t s_part[kW];
+  __shared__ uint32_t s_total, s_qn;
+
+  const uint32_t q = a.query_list[blockIdx.x];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t nl = a.nlists;
+  for (uint32_t k = tid; k < kFWords + TSLOTS; k += BLOCK) s_dyn[k] = 0;
+  if (tid == 0) s_qn = 0;
+  uint32_t len = 0;
+  if (tid < nl) {
+    s_beg[tid] = a.list_beg[(size_t)q * nl + tid];
+    len = a.list_len[(size_t)q * nl + tid];
   }
-  // pad to a multiple of 16 with values above every bin (ranks unaffected)
-  for (uint32_t e = total + tid; e < ((total + 15) & ~15u); e += BLOCK) s_emit[e] = 0xFFFFFFFFu;
+  const uint32_t excl = BlockExclusiveScan(len, s_part, &s_total);
+  if (tid < nl) {
+    s_off[tid] = excl;
+    for (uint32_t c = (excl + 63) >> 6; (c << 6) < excl + len && c < kChunks; ++c) s_cfirst[c] = (uint8_t)tid;
+  }
+  if (tid == 0) s_off[nl] = s_total;
   __syncthreads();
-  // rank of element e = number of smaller ones; four lanes per element, each
-  // counting a quarter of the array with 128-bit reads
-  uint32_t *os = a.slots + (size_t)q * a.slot_cap;
-  const uint32_t n16 = (total + 15) >> 4;  // 16-element blocks
-  for (uint32_t base4 = 0; base4 < total * 4; base4 += BLOCK) {
-    const uint32_t t4 = base4 + tid;
-    const uint32_t e = t4 >> 2, part = t4 & 3;
-    const uint32_t b = e < total ? s_emit[e] : 0u;
-    uint32_t rank = 0;
-    if (e < total) {
-      for (uint32_t blk = 0; blk < n16; ++blk) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(s_emit + blk * 16 + part * 4);
-        rank += (v.x < b) + (v.y < b) + (v.z < b) + (v.w < b);
+  const uint32_t n = s_off[nl];
+
+  // 1. gather: chunk c = wave + kW * e (64 entries of the concatenated lists),
+  //    lane = entry within the chunk; bins stay in registers
+  uint32_t bin[KE];
+#pragma unroll
+  for (uint32_t e0 = 0; e0 < KE; e0 += 4) {
+    uint32_t pos[4], prv[4], lst[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) {
+      const uint32_t c = wave + kW * (e0 + u), i = (c << 6) + lane;
+      pos[u] = 0;
+      prv[u] = kNone;
+      lst[u] = kNone;
+      if (i < n) {
+        uint32_t j = s_cfirst[c];
+        while (s_off[j + 1] <= i) ++j;
+        const uint32_t r = i - s_off[j];
+        pos[u] = a.positions[s_beg[j] + r];
+        lst[u] = j;
+        if (lane == 0 && r > 0) prv[u] = a.positions[s_beg[j] + r - 1];
       }
     }
-    rank += __shfl_xor(rank, 1);
-    rank += __shfl_xor(rank, 2);
-    if (e < total && part == 0) os[rank] = b << a.log_region;
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) {
+      const uint32_t j = lst[u];
+      const uint32_t pj = __shfl_up(j, 1), pp = __shfl_up(pos[u], 1);
+      uint32_t prev_pos = prv[u];
+      if (lane > 0 && pj == j) prev_pos = pp;
+      uint32_t x = kNone;
+      if (j != kNone) {
+        const uint32_t d0 = j * a.shift;
+        const uint32_t b = (pos[u] - d0) >> a.log_region;
+        const bool dup = prev_pos != kNone && ((prev_pos - d0) >> a.log_region) == b;
+        if (!dup) {
+          x = b;
+          const uint32_t cell = b & (FSLOTS - 1), sh = (cell & 15) * 2;
+          const uint32_t old = atomicOr(&s_flt[cell >> 4], 1u << sh);
+          if ((old >> sh) & 1u) atomicOr(&s_flt[cell >> 4], 2u << sh);
+        }
+      }
+      bin[e0 + u] = x;
+    }
   }
+  __syncthreads();
+
+  // 2. filter, then per-wave compaction into the queue
+  auto cell = [&](uint32_t b) { const uint32_t c = b & (FSLOTS - 1); return s_flt[c >> 4] >> ((c & 15) * 2); };
+  uint32_t need = 0, wave_n = 0;
+#pragma unroll
+  for (uint32_t e = 0; e < KE; ++e) {
+    const uint32_t x = bin[e];
+    bool nd = false;
+    if (x != kNone) nd = x <= 1 || ((cell(x) >> 1) & 1u) || (cell(x - 1) & 1u) || (cell(x + 1) & 1u);
+    need |= (nd ? 1u : 0u) << e;
+    wave_n += (uint32_t)__popcll(__ballot(nd));
+  }
+  uint32_t qbase = 0;
+  if (lane == 0) qbase = atomicAdd(&s_qn, wave_n);
+  qbase = (uint32_t)__shfl((int)qbase, 0);
+#pragma unroll
+  for (uint32_t e = 0; e < KE; ++e) {
+    const bool nd = (need >> e) & 1u;
+    const unsigned long long m = __ballot(nd);
+    const uint32_t at = qbase + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+    if (nd && at < QCAP) s_q[at] = bin[e];
+    qbase += (uint32_t)__popcll(m);
+  }
+  __syncthreads();
+  const uint32_t qn = s_qn;
+  if (qn > QCAP) {  // block-uniform: redone by k_seed_hash
+    if (tid == 0) a.counts[q] = kOverflow;
+    return;
+  }
+
+  // 3. exact counts of the kept entries
+  BinTable<TSLOTS> table{s_tab};
+  for (uint32_t k = tid; k < qn; k += BLOCK) table.Insert(s_q[k]);
+  __syncthreads();
+  EmitFromTable<BLOCK, TSLOTS>(a, q, s_tab, s_emit, s_part, &s_total);
 }
 
 // Slot -> compact copy for queries whose candidates fit their slot.
@@ -1588,6 +1734,14 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
 }
 
 // ------------------------------------------------------------------ K4 merge
+// One 24-byte record per selected hit, subject-relative like the reference's
+// rebase after TraceBack (aligner.cpp:710-716), with its DB chunk.
+struct SlotHit {
+  uint32_t sid, score, start, end, ml, chunk;
+};
+
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;  // sel_from: a new candidate; tb_qid: no K3 request
+
 struct MergeArgs {
   const uint32_t *group_first;         // [ng] first query of the name group
   const uint32_t *group_last;          // [ng] last query (the printed index)
@@ -1608,7 +1762,27 @@ struct MergeArgs {
   uint32_t *tb_qid;                    // [ng*cap] K3 request (0xFFFFFFFF = empty)
   uint32_t *tb_end;                    // [ng*cap]
   uint32_t wave_cap;                   // k_merge_wave: largest group kept in LDS (<= kMergeCap)
+  // the batch's candidate range (absolute): a group's candidates are its
+  // queries' candidates clipped to it (a batch may cut a name group)
+  unsigned long long cand_lo, cand_hi;
+  // results kept from earlier batches / DB chunks (reference result_list, merged
+  // again with every batch, aligner.cpp:738-741): per group carry_count[g]
+  // records at carry[g*cap]; null = none. sel_from[g*cap+k] = the carried
+  // record a selected slot repeats, or kNoSlot for a new candidate.
+  const uint32_t *carry_count;
+  const SlotHit *carry;
+  uint32_t *sel_from;
 };
+
+// A group's candidates in the batch: [*b, *b + *n) batch-relative.
+__device__ inline void GroupRange(const MergeArgs &a, uint32_t g, unsigned long long *b, unsigned long long *n) {
+  const uint32_t q0 = a.group_first[g], q1 = a.group_last[g];
+  unsigned long long lo = a.offsets[q0], hi = a.offsets[q1] + a.counts[q1];
+  lo = lo < a.cand_lo ? a.cand_lo : (lo > a.cand_hi ? a.cand_hi : lo);
+  hi = hi < a.cand_lo ? a.cand_lo : (hi > a.cand_hi ? a.cand_hi : hi);
+  *b = lo - a.out_base;
+  *n = hi - lo;
+}
 
 // DB::GetID (db.h:106-135), unsigned arithmetic as the reference.
 __device__ inline uint32_t SubjectOf(const uint32_t *starts, uint32_t n, uint32_t len, uint32_t p) {
@@ -1629,36 +1803,53 @@ struct ScoreDescending {
 };
 
 // One name group's selection on one thread (k_merge; k_merge_wave's fallback).
+// The group's list is the reference's l: the batch's candidates in query order,
+// then the carried results (aligner.cpp:732-741); carried entries are taken
+// unchanged and do not claim their subject (aligner.cpp:719-721).
 __device__ inline void MergeGroup(const MergeArgs &a, uint32_t g) {
-  const uint32_t q0 = a.group_first[g], q1 = a.group_last[g];
-  const unsigned long long b = a.offsets[q0] - a.out_base;
-  const unsigned long long n = a.offsets[q1] + a.counts[q1] - a.out_base - b;
-  unsigned long long *keys = a.keys + b;
+  unsigned long long b, n;
+  GroupRange(a, g, &b, &n);
+  const uint32_t nc = a.carry_count ? a.carry_count[g] : 0u;
+  const size_t so = (size_t)g * a.cap;
+  unsigned long long *keys = a.keys + b + so;  // scratch: the group's n + cap keys
   for (unsigned long long i = 0; i < n; ++i)
     keys[i] = ((unsigned long long)a.score[b + i] << 32) | (uint32_t)i;
+  for (uint32_t k = 0; k < nc; ++k)
+    keys[n + k] = ((unsigned long long)a.carry[so + k].score << 32) | (uint32_t)(n + k);
+  const unsigned long long total = n + nc;
   // std::sort's order, finalized lazily: the walk usually stops long before
   // the whole group is sorted
-  stdsort::LazySort<unsigned long long, ScoreDescending> order(keys, (long)n, ScoreDescending());
-  uint32_t *sid_out = a.sel_sid + (size_t)g * a.cap;
-  uint32_t *cand_out = a.sel_cand + (size_t)g * a.cap;
+  stdsort::LazySort<unsigned long long, ScoreDescending> order(keys, (long)total, ScoreDescending());
+  uint32_t *sid_out = a.sel_sid + so;
+  uint32_t *cand_out = a.sel_cand + so;
   uint32_t count = 0;
-  for (unsigned long long i = 0; i < n; ++i) {
+  for (unsigned long long i = 0; i < total; ++i) {
     while ((long)i >= order.done) order.Advance();
-    const unsigned long long c = b + (uint32_t)keys[i];
-    const uint32_t sid = SubjectOf(a.subj_start, a.nsubj, a.dblen, a.end[c]);
-    bool seen = false;
-    for (uint32_t k = 0; k < count; ++k) seen |= sid_out[k] == sid;
-    if (!seen) {
-      sid_out[count] = sid;
-      cand_out[count] = (uint32_t)c;
-      a.tb_qid[(size_t)g * a.cap + count] = a.cand_qid[a.out_base + c];
-      a.tb_end[(size_t)g * a.cap + count] = a.end[c];
+    const uint32_t idx = (uint32_t)keys[i];
+    if (idx >= n) {  // a carried result: kept as it is
+      sid_out[count] = kNoSlot;
+      cand_out[count] = kNoSlot;
+      if (a.sel_from) a.sel_from[so + count] = idx - (uint32_t)n;
+      a.tb_qid[so + count] = kNoSlot;
       ++count;
+    } else {
+      const unsigned long long c = b + idx;
+      const uint32_t sid = SubjectOf(a.subj_start, a.nsubj, a.dblen, a.end[c]);
+      bool seen = false;
+      for (uint32_t k = 0; k < count; ++k) seen |= sid_out[k] == sid;
+      if (!seen) {
+        sid_out[count] = sid;
+        cand_out[count] = (uint32_t)c;
+        if (a.sel_from) a.sel_from[so + count] = kNoSlot;
+        a.tb_qid[so + count] = a.cand_qid[a.out_base + c];
+        a.tb_end[so + count] = a.end[c];
+        ++count;
+      }
     }
     if (count >= a.best) break;
   }
   a.sel_count[g] = count;
-  for (uint32_t k = count; k < a.cap; ++k) a.tb_qid[(size_t)g * a.cap + k] = 0xFFFFFFFFu;
+  for (uint32_t k = count; k < a.cap; ++k) a.tb_qid[so + k] = kNoSlot;
 }
 
 __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
@@ -1766,23 +1957,25 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_merge_wave(MergeArgs a) {
   const uint32_t lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t g = blockIdx.x * kMergeWaves + w;
   if (g >= a.ng) return;
-  const uint32_t q0 = a.group_first[g], q1 = a.group_last[g];
-  const unsigned long long b = a.offsets[q0] - a.out_base;
-  const unsigned long long n64 = a.offsets[q1] + a.counts[q1] - a.out_base - b;
-  if (n64 > a.wave_cap) {
+  unsigned long long b, n64;
+  GroupRange(a, g, &b, &n64);
+  const size_t so = (size_t)g * a.cap;
+  const uint32_t nc = a.carry_count ? a.carry_count[g] : 0u;
+  if (n64 + nc > a.wave_cap) {
     if (lane == 0) MergeGroup(a, g);
     return;
   }
-  const uint32_t n = (uint32_t)n64;
+  const uint32_t nnew = (uint32_t)n64, n = nnew + nc;
   unsigned long long *K = s_key[w];
-  for (uint32_t i = lane; i < n; i += 64) K[i] = ((unsigned long long)a.score[b + i] << 32) | i;
+  for (uint32_t i = lane; i < nnew; i += 64) K[i] = ((unsigned long long)a.score[b + i] << 32) | i;
+  for (uint32_t k = lane; k < nc; k += 64)
+    K[nnew + k] = ((unsigned long long)a.carry[so + k].score << 32) | (nnew + k);
   MergeFrame *stk = s_stack[w];
   uint32_t *taken = s_taken[w];
   if (lane == 0 && n) stk[0] = MergeFrame{0u, n, 2 * stdsort::Lg((long)n)};
   int sp = n ? 1 : 0;
   WaveSync();
   const ScoreDescending less;
-  const size_t so = (size_t)g * a.cap;
   uint32_t count = 0, walked = 0, done = 0;
   while (count < a.best && walked < n) {
     if (walked == done) {
@@ -1810,18 +2003,24 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_merge_wave(MergeArgs a) {
       WaveSync();
       done = f.last;
     }
-    // the walk over finalized keys, up to 64 at a time, in order
+    // the walk over finalized keys, up to 64 at a time, in order; a carried
+    // result is taken unchanged and claims no subject (sid kNoSlot matches no
+    // real subject)
     const uint32_t m = min(64u, done - walked);
-    uint32_t sid = 0xFFFFFFFFu, c = 0;
-    bool ok = lane < m;
+    uint32_t sid = kNoSlot, c = 0, idx = 0;
+    bool ok = lane < m, carried = false;
     if (ok) {
-      c = (uint32_t)(b + (uint32_t)K[walked + lane]);
-      sid = SubjectOf(a.subj_start, a.nsubj, a.dblen, a.end[c]);
-      for (uint32_t k = 0; k < count; ++k) ok = ok && taken[k] != sid;
+      idx = (uint32_t)K[walked + lane];
+      carried = idx >= nnew;
+      if (!carried) {
+        c = (uint32_t)(b + idx);
+        sid = SubjectOf(a.subj_start, a.nsubj, a.dblen, a.end[c]);
+        for (uint32_t k = 0; k < count; ++k) ok = ok && taken[k] != sid;
+      }
     }
     for (uint32_t t = 0; t + 1 < m; ++t) {
       const uint32_t st = (uint32_t)__shfl((int)sid, (int)t);
-      if (lane > t && st == sid) ok = false;
+      if (!carried && lane > t && st == sid) ok = false;
     }
     const unsigned long long bal = __ballot(ok);
     const uint32_t rank = __popcll(bal & ((1ull << lane) - 1));
@@ -1829,9 +2028,16 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_merge_wave(MergeArgs a) {
     if (ok && rank < take) {
       const uint32_t at = count + rank;
       a.sel_sid[so + at] = sid;
-      a.sel_cand[so + at] = c;
-      a.tb_qid[so + at] = a.cand_qid[a.out_base + c];
-      a.tb_end[so + at] = a.end[c];
+      if (carried) {
+        a.sel_cand[so + at] = kNoSlot;
+        a.sel_from[so + at] = idx - nnew;
+        a.tb_qid[so + at] = kNoSlot;
+      } else {
+        a.sel_cand[so + at] = c;
+        if (a.sel_from) a.sel_from[so + at] = kNoSlot;
+        a.tb_qid[so + at] = a.cand_qid[a.out_base + c];
+        a.tb_end[so + at] = a.end[c];
+      }
       taken[at] = sid;
     }
     WaveSync();
@@ -1842,22 +2048,23 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_merge_wave(MergeArgs a) {
   for (uint32_t k = count + lane; k < a.cap; k += 64) a.tb_qid[so + k] = 0xFFFFFFFFu;
 }
 
-// One 20-byte record per selected hit, subject-relative like the reference's
-// rebase after TraceBack (aligner.cpp:710-716).
-struct SlotHit {
-  uint32_t sid, score, start, end, ml;
-};
-
+// Selected slots -> records: a new hit rebased to its subject after K3, a
+// carried one copied (sel_from), so out[] is the group's new result list.
 __global__ void k_finalize(const uint32_t *sel_count, const uint32_t *sel_cand,
                            const uint32_t *sel_sid, const uint32_t *score, const uint32_t *end,
                            const uint32_t *tb_start, const uint32_t *tb_ml,
-                           const uint32_t *subj_start, uint32_t ng, uint32_t cap, SlotHit *out) {
+                           const uint32_t *subj_start, uint32_t ng, uint32_t cap, uint32_t chunk,
+                           const uint32_t *sel_from, const SlotHit *carry, SlotHit *out) {
   const size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= (size_t)ng * cap) return;
   const uint32_t g = (uint32_t)(s / cap), k = (uint32_t)(s - (size_t)g * cap);
   if (k >= sel_count[g]) return;
+  if (sel_from && sel_from[s] != kNoSlot) {
+    out[s] = carry[(size_t)g * cap + sel_from[s]];
+    return;
+  }
   const uint32_t c = sel_cand[s], sid = sel_sid[s], pos = subj_start[sid];
-  out[s] = SlotHit{sid, score[c], tb_start[s] - pos, end[c] - pos, tb_ml[s]};
+  out[s] = SlotHit{sid, score[c], tb_start[s] - pos, end[c] - pos, tb_ml[s], chunk};
 }
 
 // The gathered hit record (include/ghostm_hip.h GhostmHit), written on the
@@ -1868,16 +2075,17 @@ struct HitRecord32 {
   float seq_id;
 };
 
+// chunk_base[c]: global index of DB chunk c's first subject
 __global__ void k_records(const uint32_t *sel_count, const SlotHit *slots, const uint32_t *prefix,
                           const uint32_t *group_last, uint32_t ng, uint32_t cap, uint32_t q_base,
-                          uint32_t d_base, HitRecord32 *out) {
+                          const uint32_t *chunk_base, HitRecord32 *out) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= ng) return;
   const uint32_t n = sel_count[g], at = prefix[g], qid = q_base + group_last[g];
   for (uint32_t k = 0; k < n; ++k) {
     const SlotHit h = slots[(size_t)g * cap + k];
     const uint32_t len = h.ml >> 8, match = h.ml & 0xFFu;
-    out[at + k] = HitRecord32{qid, d_base + h.sid, h.score, h.start, h.end, len, match,
+    out[at + k] = HitRecord32{qid, chunk_base[h.chunk] + h.sid, h.score, h.start, h.end, len, match,
                               (float)match / (float)len};
   }
 }

@@ -68,6 +68,8 @@ class GhostmStats(ctypes.Structure):
         ("seed_queries_class", c_uint64 * 4),
         ("seed_queries_wide", c_uint64),
         ("segments", c_uint64),
+        ("seed_runs_filter", c_uint64),
+        ("seed_filter_overflows", c_uint64),
     ]
 
     def as_dict(self) -> dict:

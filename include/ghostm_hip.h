@@ -161,6 +161,8 @@ typedef struct GhostmStats {
   uint64_t seed_queries_class[4];   /* K1 queries per size class by list entries (3 = global merge) */
   uint64_t seed_queries_wide;       /* K1 queries with more candidates than a slot (offset pass) */
   uint64_t segments;                /* device-merge segments (K2 -> K4 -> K3 rounds) */
+  uint64_t seed_runs_filter;        /* K1 runs whose classes 0/1 used the presence-filtered table */
+  uint64_t seed_filter_overflows;   /* ... queries whose filter queue overflowed (redone unfiltered) */
 } GhostmStats;
 
 /* Session: parse `aln` options exactly like the reference (getopt string

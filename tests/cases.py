@@ -160,6 +160,7 @@ VARIANTS = [
     ("syn_chunks", "default", [], {}),
     ("syn_chunks", "S1", ["-S", "1"], {}),
     ("syn_chunks", "L0", ["-L", "0"], {}),
+    ("syn_chunks", "b20_y2", ["-b", "20", "-y", "2"], {}),
     ("syn_scale", "default", [], {}),
     ("syn_repeat", "default", [], {}),
     ("syn_repeat", "b20_y2", ["-b", "20", "-y", "2"], {}),
@@ -184,6 +185,11 @@ BATCH_VARIANTS = [
     ("syn_small", "cut700", [], {"GHOSTM_MAX_LIST_OVERRIDE": "700"}),
     ("syn_dna", "cut100", [], {"GHOSTM_MAX_LIST_OVERRIDE": "100"}),
     ("syn_dna", "cut13", ["-y", "2"], {"GHOSTM_MAX_LIST_OVERRIDE": "13"}),
+    # -b above std::sort's insertion threshold (16): the carried result lists are
+    # re-sorted by introsort every batch, so tie order matters across batches
+    ("syn_small", "cut300_b20", ["-b", "20", "-y", "2"], {"GHOSTM_MAX_LIST_OVERRIDE": "300"}),
+    ("syn_repeat", "cut2000_b20", ["-b", "20"], {"GHOSTM_MAX_LIST_OVERRIDE": "2000"}),
+    ("syn_dna", "cut57_b3", ["-b", "3"], {"GHOSTM_MAX_LIST_OVERRIDE": "57"}),
 ]
 
 

@@ -43,17 +43,43 @@ def test_gpu_matches_reference_golden(ds, var, opts, env, dataset, golden, tmp_p
     assert cases.sha256(str(tmp_path / "g.out")) == want["sha256"]
 
 
+@pytest.mark.parametrize("merge", ["device", "device_thread", "host"])
 @pytest.mark.parametrize("ds,var,opts,env", cases.BATCH_VARIANTS,
                          ids=[f"{v[0]}/{v[1]}" for v in cases.BATCH_VARIANTS])
-def test_gpu_batch_cuts_match_oracle(ds, var, opts, env, dataset, tmp_path):
+def test_gpu_batch_cuts_match_oracle(merge, ds, var, opts, env, dataset, tmp_path):
     """CPU-path batch semantics (carry, drop of a carried last query, stop at the
-    first empty batch) at tiny -l, against the oracle."""
+    first empty batch) at tiny -l, against the oracle: on the device (K4 merges
+    every batch's candidates with the carried result lists, wave and one-thread
+    kernels) and with the host merge (GHOSTM_MERGE=host)."""
     d = dataset(ds)
+    env = dict(env)
+    if merge == "host":
+        env["GHOSTM_MERGE"] = "host"
+    elif merge == "device_thread":
+        env["GHOSTM_K4"] = "thread"
     text, st = _gpu_text(d, opts, env, str(tmp_path / "g.out"))
-    want = cases.run_aln(cases.ORACLE, d, opts, env, str(tmp_path / "o.out"))
+    want = cases.run_aln(cases.ORACLE, d, opts, {k: v for k, v in env.items() if k.startswith("GHOSTM_MAX")},
+                         str(tmp_path / "o.out"))
     assert text == want
     if env.get("GHOSTM_MAX_LIST_OVERRIDE") not in ("1",):
         assert st["batches"] > 1
+    if merge == "host" or st["batches"] == 0:
+        assert st["merge_launches"] == 0
+    else:
+        assert st["merge_launches"] > 0
+
+
+@pytest.mark.parametrize("merge", ["device", "host"])
+@pytest.mark.parametrize("var,opts", [("default", []), ("b20_y2", ["-b", "20", "-y", "2"]), ("S1", ["-S", "1"])])
+def test_multi_db_chunk_merge(merge, var, opts, dataset, golden, tmp_path):
+    """Three DB chunks: the result lists carried from chunk to chunk are merged
+    on the device (K4) or on the host, both equal to the reference."""
+    d = dataset("syn_chunks")
+    env = {"GHOSTM_MERGE": "host"} if merge == "host" else {}
+    text, st = _gpu_text(d, opts, env, str(tmp_path / "g.out"))
+    (tmp_path / "g.out").write_bytes(text)
+    assert cases.sha256(str(tmp_path / "g.out")) == golden["aln"][f"syn_chunks/{var}"]["sha256"]
+    assert (st["merge_launches"] == 0) if merge == "host" else (st["merge_launches"] > 0)
 
 
 def test_cli_aln_writes_same_file(dataset, golden, tmp_path):
