@@ -19,6 +19,8 @@ GOLDEN = os.path.join(HERE, "golden")
 GHOSTM = os.path.join(REPO, "ghostm_amd", "bin", "ghostm")
 ORACLE = os.path.join(REPO, "oracle", "_build", "ghostm_oracle")
 REF = os.path.join(REPO, "oracle", "_ref", "ghostm_ref")
+# the same reference objects linked against libghostm_hip.so (the drop-in), not a trap stub
+REF_PLUGIN = os.path.join(REPO, "oracle", "_ref", "ghostm_ref_plugin")
 PAM250 = os.path.join(GOLDEN, "matrices", "PAM250")
 PAM30 = os.path.join(GOLDEN, "matrices", "pam30_name", "PAM30")
 

@@ -36,18 +36,38 @@ def test_hit_record_layout():
 
 
 def test_reference_host_links_against_plugin():
-    """Where the reference was compiled here, its binary resolves the ten plugin
-    symbols from libghostm_hip.so (drop-in at the symbol level)."""
+    """Where the reference was compiled here, ghostm_ref_plugin resolves the ten
+    plugin symbols from libghostm_hip.so (drop-in at the symbol level), while the
+    oracle build ghostm_ref does not link the product at all."""
+    if not os.path.exists(cases.REF_PLUGIN):
+        import pytest
+
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    out = subprocess.run(["ldd", cases.REF_PLUGIN], capture_output=True, text=True, check=True).stdout
+    assert "libghostm_hip.so" in out
+    und = subprocess.run(["nm", "-D", "--undefined-only", cases.REF_PLUGIN], capture_output=True,
+                         text=True, check=True).stdout
+    for s in ["SearchNextGpu", "CalculateScoreGpu", "SetDbGpu", "SetQueryGpu"]:
+        assert s in und
+    out = subprocess.run(["ldd", cases.REF], capture_output=True, text=True, check=True).stdout
+    assert "libghostm_hip.so" not in out and "libamdhip64" not in out
+
+
+def test_reference_oracle_traps_gpu_path(tmp_path):
+    """The oracle build's GPU symbols are the exit(2) trap stub (oracle/gpu_trap.c):
+    asking it for -D fails loudly instead of running anything."""
     if not os.path.exists(cases.REF):
         import pytest
 
         pytest.skip("oracle/_ref not built (no /root/reference here)")
-    out = subprocess.run(["ldd", cases.REF], capture_output=True, text=True, check=True).stdout
-    assert "libghostm_hip.so" in out
-    und = subprocess.run(["nm", "-D", "--undefined-only", cases.REF], capture_output=True,
-                         text=True, check=True).stdout
-    for s in ["SearchNextGpu", "CalculateScoreGpu", "SetDbGpu", "SetQueryGpu"]:
-        assert s in und
+    d = tmp_path
+    subprocess.run([cases.GHOSTM, "qry", "-i", os.path.join(cases.GOLDEN, "testset_queries.fasta"),
+                    "-o", str(d / "q")], check=True, capture_output=True)
+    subprocess.run([cases.GHOSTM, "db", "-i", os.path.join(cases.GOLDEN, "testset_db.fasta"),
+                    "-o", str(d / "db")], check=True, capture_output=True)
+    r = subprocess.run([cases.REF, "aln", "-i", str(d / "q"), "-d", str(d / "db"), "-o", str(d / "o"),
+                        "-D", "0"], capture_output=True)
+    assert r.returncode == 2 and b"called in the CPU oracle build" in r.stderr
 
 
 def test_cli_usage_and_unknown_command(built):

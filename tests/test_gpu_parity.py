@@ -265,16 +265,16 @@ REF_GPU_VARIANTS = [v for v in cases.VARIANTS
                                             "syn_short/default")]
 
 
-@pytest.mark.skipif(not os.path.exists(cases.REF), reason="reference build (oracle/_ref) absent")
+@pytest.mark.skipif(not os.path.exists(cases.REF_PLUGIN), reason="reference build (oracle/_ref) absent")
 @pytest.mark.parametrize("ds,var,opts,env", REF_GPU_VARIANTS, ids=[f"{v[0]}/{v[1]}" for v in REF_GPU_VARIANTS])
 def test_reference_driver_on_this_plugin(ds, var, opts, env, dataset, golden, tmp_path):
     """The drop-in itself: the reference's own aligner.cpp (oracle/_ref, compiled from
-    the reference sources and linked against libghostm_hip.so) run with -D 0 drives
+    the reference sources, ghostm_ref_plugin: linked against libghostm_hip.so) run with -D 0 drives
     this repo's HIP kernels through the reference plugin ABI (InitGpu ... SearchNextGpu,
     CalculateScoreGpu ... FreeGpu) and must print the reference CPU path's bytes."""
     d = dataset(ds)
     out = str(tmp_path / "ref_gpu.out")
-    cases.run_aln(cases.REF, d, list(opts) + ["-D", "0"], env, out)
+    cases.run_aln(cases.REF_PLUGIN, d, list(opts) + ["-D", "0"], env, out)
     assert cases.sha256(out) == golden["aln"][f"{ds}/{var}"]["sha256"]
 
 
