@@ -4,6 +4,7 @@
 #include <getopt.h>
 
 #include <algorithm>
+#include <atomic>
 #include <charconv>
 #include <climits>
 #include <cmath>
@@ -17,6 +18,45 @@
 #include "common.h"
 
 namespace ghostm {
+
+// ------------------------------------------------------------------ trace
+namespace {
+struct TraceEvent {
+  double t;
+  const char *label;
+  uint64_t value;
+  std::thread::id thread;
+};
+std::mutex g_trace_mu;
+std::vector<TraceEvent> g_trace;
+}  // namespace
+
+bool TraceOn() {
+  static const bool on = [] {
+    const char *e = getenv("GHOSTM_TRACE");
+    return e && *e && strcmp(e, "0") != 0;
+  }();
+  return on;
+}
+
+void TraceMark(const char *label, uint64_t value) {
+  if (!TraceOn()) return;
+  const double t = NowSeconds();
+  std::lock_guard<std::mutex> lk(g_trace_mu);
+  g_trace.push_back(TraceEvent{t, label, value, std::this_thread::get_id()});
+}
+
+void TraceDump() {
+  if (!TraceOn()) return;
+  std::lock_guard<std::mutex> lk(g_trace_mu);
+  if (g_trace.empty()) return;
+  const double t0 = g_trace.front().t;
+  const std::thread::id main = g_trace.front().thread;
+  for (const TraceEvent &e : g_trace)
+    fprintf(stderr, "trace %9.3f %s %-18s %llu\n", (e.t - t0) * 1e3, e.thread == main ? "M" : "F", e.label,
+            (unsigned long long)e.value);
+  g_trace.clear();
+}
 
 unsigned HostThreads() {
   if (const char *e = getenv("GHOSTM_THREADS")) {
@@ -506,13 +546,15 @@ void Session::DevicePass(QueryData &q, DbData &d, const std::vector<uint32_t> &c
     // their lists are printed straight from the carry
     const bool identity = c1 == c0 && carry_in && opt_.best <= 16;
     const bool work = c1 > c0 || (carry_in && !identity);
+    TraceMark("seg", k);
     if (c1 > c0) {
       // the next segment's K2 tasks are built while this one's K2 runs
       dev.Score(q.dev, d.dev, c0, c1 - c0, segs[k].q_first, segs[k].q_end, counts, offsets, base, gap, nullptr,
                 nullptr, k + 1 < segs.size() ? &segs[k + 1] : nullptr);
     }
+    TraceMark("score_done", c1 - c0);
     auto sel_counts = std::make_shared<std::vector<uint32_t>>();
-    auto sel_hits = std::make_shared<std::vector<SelectedHit>>();
+    auto sel_hits = std::make_shared<HostHits>();
     const double t0 = NowSeconds();
     if (work) {
       dev.MergeSelect(q.dev, d.dev, g0, g1, c0, c1 - c0, opt_.best, tb_base, opt_.open_gap, opt_.extend_gap,
@@ -524,14 +566,18 @@ void Session::DevicePass(QueryData &q, DbData &d, const std::vector<uint32_t> &c
     }
     stats_.seconds_merge += NowSeconds() - t0;
     stats_.segments += 1;
+    TraceMark("merge_done", g1 - g0);
     if (!final_pass) continue;
     if (work || identity) dev.AppendRecords(q.dev, g0, *sel_counts, cap, q.global_base, identity);
     Part *part = NewPart();
     const QueryData *qp = &q;
-    formatter_->Submit([this, qp, g0, sel_counts, sel_hits, cap, part] {
+    TraceMark("records", k);
+    formatter_->Submit([this, qp, g0, sel_counts, sel_hits, cap, part, k] {
       const double t = NowSeconds();
+      TraceMark("fmt_begin", k);
       FormatSelected(*qp, g0, *sel_counts, *sel_hits, cap, part);
       stats_.seconds_output += NowSeconds() - t;
+      TraceMark("fmt_end", k);
     });
   }
 }
@@ -559,8 +605,10 @@ void Session::RunQueryChunk(QueryData &q) {
   for (size_t di = 0; di < dbs_.size(); ++di) {
     DbData &d = dbs_[di];
     sc.seed_mask = d.chunk.seed;
+    TraceMark("seed", q.chunk.nseq);
     const uint64_t total = dev.Seed(q.dev, d.dev, sc, &counts, &offsets);
     stats_.candidates += total;
+    TraceMark("seed_done", total);
     const std::vector<Batch> batches = CpuBatches(counts, opt_.max_list_length);
     for (size_t bi = 0; bi < batches.size(); ++bi) {
       const Batch &b = batches[bi];
@@ -576,7 +624,7 @@ void Session::RunQueryChunk(QueryData &q) {
   if (!formatted) {
     // the last DB chunk had no batch: the carried lists are the results
     auto sel_counts = std::make_shared<std::vector<uint32_t>>();
-    auto sel_hits = std::make_shared<std::vector<SelectedHit>>();
+    auto sel_hits = std::make_shared<HostHits>();
     dev.CarryToHost(q.dev, 0, (uint32_t)q.group_first.size(), cap, sel_counts.get(), sel_hits.get());
     records_on_device_ = false;  // records are uploaded from the host on demand
     Part *part = NewPart();
@@ -687,6 +735,16 @@ struct LineFormat {
   std::vector<std::string> bits_txt;  // per score
   std::vector<double> expd;           // per score: exp(-1.0 * s * lambda)
   std::vector<std::string> id_txt;    // per (len, match): 100*id (style 0) or id (style 2)
+  // E-value text per (query length, score): the E-value depends on nothing
+  // else (search space = qlen x the DB's residue sum), so each one is formatted
+  // once per session, by whichever formatter thread needs it first. Entry:
+  // byte 0 = text length (0: not yet), bytes 1..15 = the text; racing writers
+  // store the same bytes.
+  struct EvText {
+    std::atomic<uint64_t> a{0}, b{0};
+  };
+  static constexpr uint32_t kEvScores = 4096;
+  mutable std::unique_ptr<EvText[]> ev_txt;
 
   LineFormat(int st, const KarlinParams &k, uint32_t max_score) : style(st), ev(k) {
     if (style == 0) {
@@ -696,6 +754,7 @@ struct LineFormat {
         bits_txt[sc] = FloatText(ev.Bits((int)sc));
         expd[sc] = exp(static_cast<double>(-1.0 * (int)sc * ev.p.lambda));
       }
+      ev_txt.reset(new EvText[(size_t)(kMaxQueryLength + 1) * kEvScores]);
     }
     if (style != 1) {
       id_txt.resize(kIdLen * kIdMatch);
@@ -711,11 +770,33 @@ struct LineFormat {
     if (len < kIdLen && m < kIdMatch && m <= len && len > 0) return PutStr(p, id_txt[len * kIdMatch + m]);
     return PutFloat(p, Id(len, m));
   }
+  // the E-value (float)((double)scaled * exp(-lambda * score)), as %g text
+  char *PutEvalue(char *p, uint32_t qlen, uint32_t score, float scaled) const {
+    const double e = score < expd.size() ? expd[score] : exp(static_cast<double>(-1.0 * (int)score * ev.p.lambda));
+    if (qlen > kMaxQueryLength || score >= kEvScores || !ev_txt) return PutFloat(p, (float)((double)scaled * e));
+    EvText &c = ev_txt[(size_t)qlen * kEvScores + score];
+    uint64_t w[2];
+    w[0] = c.a.load(std::memory_order_acquire);
+    if (w[0] == 0) {
+      char buf[16] = {0};
+      char *end = std::to_chars(buf + 1, buf + 16, (float)((double)scaled * e), std::chars_format::general, 6).ptr;
+      buf[0] = (char)(end - buf - 1);
+      std::memcpy(w, buf, 16);
+      c.b.store(w[1], std::memory_order_relaxed);
+      c.a.store(w[0], std::memory_order_release);
+    } else {
+      w[1] = c.b.load(std::memory_order_relaxed);
+    }
+    char buf[16];
+    std::memcpy(buf, w, 16);
+    std::memcpy(p, buf + 1, 15);  // the line buffer has kFixed bytes of room
+    return p + (unsigned char)buf[0];
+  }
   // bytes a line can take beyond the two names
   static constexpr size_t kFixed = 160;
-  // scaled = (float)search_space * K, per query
+  // scaled = (float)search_space * K, per query of non-X length qlen
   char *Write(char *p, const std::string &qname, const std::string &sname, uint32_t score, uint32_t start,
-              uint32_t end, uint32_t len, uint32_t match, float scaled) const {
+              uint32_t end, uint32_t len, uint32_t match, float scaled, uint32_t qlen) const {
     p = PutStr(p, qname);
     *p++ = '\t';
     p = PutStr(p, sname);
@@ -737,8 +818,7 @@ struct LineFormat {
       p = PutU32(p, match); *p++ = '\t';
       p = PutU32(p, start + 1); *p++ = '\t';
       p = PutU32(p, end + 1); *p++ = '\t';
-      const double e = score < expd.size() ? expd[score] : exp(static_cast<double>(-1.0 * (int)score * ev.p.lambda));
-      p = PutFloat(p, (float)((double)scaled * e)); *p++ = '\t';
+      p = PutEvalue(p, qlen, score, scaled); *p++ = '\t';
       if (score < bits_txt.size()) p = PutStr(p, bits_txt[score]);
       else p = PutFloat(p, ev.Bits((int)score));
       *p++ = '\t';
@@ -795,7 +875,7 @@ void Session::FormatResults(const QueryData &q, const Results &results, Part *ou
         const DbData &d = dbs_[h.db_chunk];
         const std::string &sname = d.chunk.names[h.subject];
         char *p = text.Reserve(qname.size() + sname.size() + LineFormat::kFixed);
-        text.Commit(w.Write(p, qname, sname, h.score, h.start, h.end, h.aln_len, h.aln_match, scaled));
+        text.Commit(w.Write(p, qname, sname, h.score, h.start, h.end, h.aln_len, h.aln_match, scaled, q.qlen[i]));
         hits.push_back(GhostmHit{q.global_base + (uint32_t)i, d.global_base + h.subject, h.score, h.start,
                                  h.end, h.aln_len, h.aln_match, h.seq_id});
       }
@@ -806,7 +886,7 @@ void Session::FormatResults(const QueryData &q, const Results &results, Part *ou
 // Same text from the device-selected hits: a name group's lines are printed
 // under its last query (the reference's result_list[last]).
 void Session::FormatSelected(const QueryData &q, uint32_t g0, const std::vector<uint32_t> &counts,
-                             const std::vector<SelectedHit> &hits, uint32_t cap, Part *out) {
+                             const HostHits &hits, uint32_t cap, Part *out) {
   const uint32_t ng = (uint32_t)counts.size();
   const unsigned workers = std::max(1u, threads_ > 1 ? threads_ - 1 : 1u);
   out->Reset(workers);
@@ -830,7 +910,7 @@ void Session::FormatSelected(const QueryData &q, uint32_t g0, const std::vector<
         const float seq_id = (float)match / (float)len;  // aligner.cpp:945
         const std::string &sname = d.chunk.names[h.sid];
         char *p = text.Reserve(name.size() + sname.size() + LineFormat::kFixed);
-        text.Commit(w.Write(p, name, sname, h.score, h.start, h.end, len, match, scaled));
+        text.Commit(w.Write(p, name, sname, h.score, h.start, h.end, len, match, scaled, q.qlen[i]));
         ph.push_back(GhostmHit{q.global_base + i, d.global_base + h.sid, h.score, h.start, h.end, len, match,
                                seq_id});
       }
@@ -853,13 +933,17 @@ void Session::Run() {
   dev.ResetRecords();
   records_on_device_ = true;
   const double t0 = NowSeconds();
+  TraceMark("run");
   for (QueryData &q : queries_) {
     RunQueryChunk(q);
     stats_.queries += q.chunk.nseq;
     for (uint32_t v : q.qlen) stats_.query_residues += v;
   }
+  TraceMark("drain");
   formatter_->Drain();
   stats_.seconds_total = NowSeconds() - t0;
+  TraceMark("run_end");
+  TraceDump();
   const DeviceTimes &dt = dev.times();
   stats_.seconds_seed = dt.seed;
   stats_.seconds_score = dt.score;

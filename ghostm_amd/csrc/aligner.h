@@ -150,7 +150,7 @@ class Session {
                       const std::vector<uint64_t> &offsets, Results *results);
   void FormatResults(const QueryData &q, const Results &results, Part *out);
   void FormatSelected(const QueryData &q, uint32_t g0, const std::vector<uint32_t> &counts,
-                      const std::vector<SelectedHit> &hits, uint32_t cap, Part *out);
+                      const HostHits &hits, uint32_t cap, Part *out);
   Part *NewPart();
   const LineFormat &Format();
 

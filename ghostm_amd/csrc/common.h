@@ -30,4 +30,10 @@ inline double NowSeconds() {
   return duration<double>(steady_clock::now().time_since_epoch()).count();
 }
 
+// GHOSTM_TRACE=1: a host timeline of each GhostmSessionRun (label, value,
+// thread, ms since the run started), printed to stderr when the run ends.
+bool TraceOn();
+void TraceMark(const char *label, uint64_t value = 0);
+void TraceDump();
+
 }  // namespace ghostm

@@ -11,6 +11,7 @@
 #pragma once
 #include <cstddef>
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -42,6 +43,15 @@ struct DevDb;
 // subject-relative coordinates, ml = (aln_len << 8) | matches.
 struct SelectedHit {
   uint32_t sid, score, start, end, ml, chunk;  // chunk: the hit's DB chunk
+};
+
+// Selected hits landed on the host: an uninitialised block, freed when the last
+// copy of `block` goes (the formatter releases it).
+struct HostHits {
+  std::shared_ptr<void> block;
+  SelectedHit *data = nullptr;
+  size_t n = 0;
+  const SelectedHit &operator[](size_t i) const { return data[i]; }
 };
 
 // One K4 pass: the batch's candidate range (absolute; a batch may cut a name
@@ -125,12 +135,14 @@ class DeviceModule {
   // null: nothing but the counts is copied back).
   void MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, uint64_t cand_begin, uint64_t n, uint32_t best,
                    uint32_t tb_base, int open, int ext, std::vector<uint32_t> *counts,
-                   std::vector<SelectedHit> *hits, const MergePass &pass = MergePass());
+                   HostHits *hits, const MergePass &pass = MergePass());
   // Carried result lists of a query chunk (all groups empty), and their copy to
   // the host (counts[g], hits[g * cap + k]).
   void ResetCarry(DevQuery *q, uint32_t cap);
   void CarryToHost(DevQuery *q, uint32_t g0, uint32_t g1, uint32_t cap, std::vector<uint32_t> *counts,
-                   std::vector<SelectedHit> *hits);
+                   HostHits *hits);
+  // a block of n SelectedHit slots (contents undefined)
+  void AcquireHostHits(size_t n, HostHits *out);
   // Global index of each DB chunk's first subject (hit records' db_id).
   void SetChunkBases(const uint32_t *bases, uint32_t n);
 

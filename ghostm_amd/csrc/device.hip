@@ -152,6 +152,19 @@ constexpr size_t kFilterLds1 = (65536 / 16 + 4608 + 3072) * 4;
 // K3a: the pair table (32 x 32 codes x 32 query codes, one word each) + histogram
 static constexpr size_t kScanLds = (size_t)kern::kPairWords * 4 + kern::kSortBins * 4;
 
+// Host landing of a segment's selected hits (HostHits): a fresh, uninitialised
+// heap block per segment, freed by the formatter when it is done with it.
+// Measured alternatives (cfg4, GHOSTM_TRACE timelines): a zero-filled
+// std::vector per segment costs ~3 ms of host time per 16 M-candidate segment;
+// reusing blocks from a pool (pageable or hipHostMalloc'd) made the next K1
+// launch wait 10-27 ms for the device on most chunks (426 -> 467-475 ms/step).
+void DeviceModule::AcquireHostHits(size_t n, HostHits *out) {
+  SelectedHit *p = new SelectedHit[std::max<size_t>(n, 1)];
+  out->block = std::shared_ptr<void>(p, [](void *v) { delete[] static_cast<SelectedHit *>(v); });
+  out->data = p;
+  out->n = n;
+}
+
 DeviceModule &DeviceModule::Get() {
   static DeviceModule *m = new DeviceModule();
   return *m;
@@ -460,6 +473,7 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
   I.list_len.Reserve((size_t)nq * nlists * 4);
   HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
   HIP_CHECK(hipMemsetAsync(I.counts.p, 0, (size_t)nq * 4, S(stream_)));
+  TraceMark("k1a_memset");
 
   // K1a: list segments + bin count per query
   kern::SeedListArgs la{};
@@ -476,9 +490,12 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
   la.nbins = I.nelem.as<uint32_t>();
   hipLaunchKernelGGL(kern::k_seed_lists, dim3((nq + 3) / 4), dim3(256), 0, S(stream_), la);
   HIP_CHECK(hipGetLastError());
+  TraceMark("k1a_launch");
   std::vector<uint32_t> nbins(nq);
   HIP_CHECK(hipMemcpyAsync(nbins.data(), I.nelem.p, (size_t)nq * 4, hipMemcpyDeviceToHost, S(stream_)));
+  TraceMark("k1a_enq");
   HIP_CHECK(hipStreamSynchronize(S(stream_)));
+  TraceMark("k1a_done");
 
   // size classes (queries without any position keep count 0)
   std::vector<uint32_t> cls[4];
@@ -547,7 +564,9 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
   times_.seed_launches_hash += hash ? 1 : 0;
   times_.seed_launches_filter += filter ? 1 : 0;
   HIP_CHECK(hipMemcpyAsync(counts->data(), I.counts.p, (size_t)nq * 4, hipMemcpyDeviceToHost, S(stream_)));
+  TraceMark("k1b_enq");
   HIP_CHECK(hipStreamSynchronize(S(stream_)));
+  TraceMark("k1b_done");
   if (filter) {
     // queries whose filtered queue overflowed: the unfiltered table redoes them
     std::vector<uint32_t> redo[2];
@@ -624,6 +643,7 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
     }
   }
   HIP_CHECK(hipEventRecord(I.ev1, S(stream_)));
+  TraceMark("k1c_enq");
   times_.seed += ElapsedMs(I.ev0, I.ev1) * 1e-3;
   // algorithmic bytes: query record + 2 CSR words per list + one u32 per
   // position + 8 bytes (start, query) per candidate
@@ -1069,24 +1089,24 @@ void DeviceModule::SetChunkBases(const uint32_t *bases, uint32_t n) {
 }
 
 void DeviceModule::CarryToHost(DevQuery *q, uint32_t g0, uint32_t g1, uint32_t cap, std::vector<uint32_t> *counts,
-                               std::vector<SelectedHit> *hits) {
+                               HostHits *hits) {
   Use();
   Impl &I = *impl_;
   if (g1 > q->ngroups || g0 > g1) throw Error("group range outside the chunk");
   const size_t ng = g1 - g0;
   counts->assign(ng, 0);
-  hits->assign(ng * cap, SelectedHit{});
+  AcquireHostHits(ng * cap, hits);
   if (ng == 0) return;
   HIP_CHECK(hipMemcpyAsync(counts->data(), I.carry_count.as<uint32_t>() + g0, ng * 4, hipMemcpyDeviceToHost,
                            S(stream_)));
-  HIP_CHECK(hipMemcpyAsync(hits->data(), I.carry_hits.as<kern::SlotHit>() + (size_t)g0 * cap,
+  HIP_CHECK(hipMemcpyAsync(hits->data, I.carry_hits.as<kern::SlotHit>() + (size_t)g0 * cap,
                            ng * cap * sizeof(SelectedHit), hipMemcpyDeviceToHost, S(stream_)));
   HIP_CHECK(hipStreamSynchronize(S(stream_)));
 }
 
 void DeviceModule::MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, uint64_t cand_begin, uint64_t n,
                                uint32_t best, uint32_t tb_base, int open, int ext,
-                               std::vector<uint32_t> *counts, std::vector<SelectedHit> *hits,
+                               std::vector<uint32_t> *counts, HostHits *hits,
                                const MergePass &pass) {
   Use();
   Impl &I = *impl_;
@@ -1094,7 +1114,7 @@ void DeviceModule::MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, 
   const uint32_t ng = g1 - g0;
   const uint32_t cap = std::max<uint32_t>(best, 1);
   counts->assign(ng, 0);
-  if (hits) hits->clear();
+  if (hits) *hits = HostHits();
   if (ng == 0) return;
   if (d->nsubj == 0) throw Error("DB subjects not set for the device merge");
   const size_t slots = (size_t)ng * cap;
@@ -1196,8 +1216,8 @@ void DeviceModule::MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, 
   unsigned long long cells = 0;
   HIP_CHECK(hipMemcpyAsync(counts->data(), I.sel_count.p, (size_t)ng * 4, hipMemcpyDeviceToHost, S(stream_)));
   if (hits) {  // null: the selection stays on the device (a carried pass)
-    hits->resize(slots);
-    HIP_CHECK(hipMemcpyAsync(hits->data(), I.slot_hits.p, slots * sizeof(SelectedHit), hipMemcpyDeviceToHost,
+    AcquireHostHits(slots, hits);
+    HIP_CHECK(hipMemcpyAsync(hits->data, I.slot_hits.p, slots * sizeof(SelectedHit), hipMemcpyDeviceToHost,
                              S(stream_)));
   }
   unsigned long long scan_cells = 0;
