@@ -8,6 +8,7 @@
 //                        translation 242-324, X padding 388-423)
 #include <getopt.h>
 
+#include <algorithm>
 #include <climits>
 #include <cmath>
 #include <cstring>
@@ -256,6 +257,50 @@ void SixFrames(const std::string &dna, uint32_t dna_len, std::vector<std::string
   }
 }
 
+// qry -D: the chunk's letters concatenated, coded / translated on the GPU
+// (qformat.hip), then the same files as the CPU path.
+void FormatQueryChunkGpu(const std::vector<FastaRecord> &recs, bool dna, uint32_t width, int device,
+                         const std::string &prefix) {
+  const uint32_t n = (uint32_t)recs.size();
+  std::vector<uint64_t> off(n);
+  std::vector<uint32_t> len(n);
+  uint64_t total = 0;
+  for (uint32_t r = 0; r < n; ++r) {
+    off[r] = total;
+    len[r] = (uint32_t)recs[r].seq.size();
+    total += len[r];
+  }
+  std::string raw;
+  raw.reserve(total);
+  for (const FastaRecord &r : recs) raw += r.seq;
+  // every read is cut/padded to the first read's length (query_creator.cpp:254)
+  const uint32_t dna_len = dna ? (uint32_t)recs[0].seq.size() : 0;
+  const uint32_t per = dna ? 6 : 1;
+  std::vector<uint8_t> out((size_t)n * per * width);
+  if (GhostmFormatQueriesGpu(reinterpret_cast<const uint8_t *>(raw.data()), total, off.data(), len.data(), n,
+                             width, dna ? std::max(dna_len, 1u) : 0, out.data(), device, nullptr))
+    throw Error(std::string("qry -D: ") + GhostmGetLastError());
+  {
+    std::ofstream f((prefix + ".inf").c_str(), std::ios::binary);
+    const uint32_t nout = n * per;
+    WriteRaw(f, &nout, 1);
+    WriteRaw(f, &width, 1);
+  }
+  {
+    std::ofstream f((prefix + ".nam").c_str());
+    for (const FastaRecord &r : recs)
+      for (uint32_t k = 0; k < per; ++k) f << r.name << '\n';
+  }
+  // the CPU path's over-width warning, per record (frames: dna_len / 3 letters)
+  for (const FastaRecord &r : recs) {
+    const size_t letters = dna ? dna_len / 3 : r.seq.size();
+    if (letters > width)
+      for (uint32_t k = 0; k < per; ++k) std::cerr << "warning : the length of sequence is over. " << r.name << std::endl;
+  }
+  std::ofstream f((prefix + ".seq").c_str(), std::ios::binary);
+  WriteRaw(f, out.data(), out.size());
+}
+
 }  // namespace
 
 int QueryFormatMain(int argc, char **argv) {
@@ -263,14 +308,16 @@ int QueryFormatMain(int argc, char **argv) {
   uint32_t max_concat = 1u << 27;
   uint32_t width = 75;
   bool dna = false;
+  int device = -1;  // -D d (extension): code / translate the records on GPU d
   optind = 1;
   int c;
-  while ((c = getopt(argc, argv, "i:o:l:t:L:")) >= 0) {
+  while ((c = getopt(argc, argv, "i:o:l:t:L:D:")) >= 0) {
     switch (c) {
       case 'i': in_path = optarg; break;
       case 'o': out_prefix = optarg; break;
       case 'l': width = atoi(optarg); break;
       case 'L': max_concat = atoi(optarg) * (1 << 20); break;
+      case 'D': device = atoi(optarg); break;
       case 't':
         if (strcmp(optarg, "d") == 0) dna = true;
         else if (strcmp(optarg, "p") == 0) dna = false;
@@ -324,6 +371,12 @@ int QueryFormatMain(int argc, char **argv) {
       WriteRaw(f, &max_nseq, 1);
       for (int k = 0; k < 32; ++k) WriteRaw(f, &division, 1);
       break;
+    }
+    if (device >= 0) {
+      FormatQueryChunkGpu(recs, dna, width, device, out_prefix + "_" + std::to_string(chunk));
+      const uint32_t nout = (uint32_t)recs.size() * (dna ? 6u : 1u);
+      if (max_nseq < nout) max_nseq = nout;
+      continue;
     }
     if (dna) {
       // every read is cut/padded to the first read's length (query_creator.cpp:254)

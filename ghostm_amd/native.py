@@ -102,6 +102,8 @@ SIGNATURES = {
     "TraceBackGpu": (c_int, [c_uint32, u32p, u32p, c_uint32, c_uint32, c_int, c_int, u32p, u32p, u32p, POINTER(c_float)]),
     "GhostmBuildIndexGpu": (c_int, [POINTER(ctypes.c_uint8), c_uint32, c_uint32, c_uint32, u32p, u32p, u32p, c_int,
                                     POINTER(c_float)]),
+    "GhostmFormatQueriesGpu": (c_int, [POINTER(ctypes.c_uint8), c_uint64, POINTER(c_uint64), u32p, c_uint32, c_uint32,
+                                       c_uint32, POINTER(ctypes.c_uint8), c_int, POINTER(c_float)]),
     "GhostmSessionCreate": (c_void_p, [c_int, POINTER(c_char_p)]),
     "GhostmSessionCreateShard": (c_void_p, [c_int, POINTER(c_char_p), c_int, c_int]),
     "GhostmSessionShardRange": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),

@@ -116,6 +116,20 @@ int GhostmBuildIndexGpu(const uint8_t *seq, uint32_t len, uint32_t seed, uint32_
                         uint32_t *keys_count, uint32_t *positions, uint32_t *npos, int device,
                         float *device_ms);
 
+/* The `qry` formatter's per-residue work on the GPU (replaces QueryCreator's
+ * coding, query_creator.cpp:388-423, and six-frame translation, :242-324;
+ * SURVEY.md §8 f2). raw[raw_len] = the chunk's records' letters concatenated
+ * (no newlines); record r is raw[offsets[r] .. + lengths[r]). dna_len = 0:
+ * protein, records[n * width] = each record's residue codes, cut at or X-padded
+ * to width. dna_len > 0: DNA reads cut/padded to dna_len letters (the reference
+ * uses the chunk's first read length), records[6n * width] = per read the
+ * frames +0 +1 +2 and the reverse complement's +0 +1 +2 with stop codons
+ * masked to '*' until the next ATG, each cut/X-padded to width. Byte-identical
+ * to the CPU formatter's .seq. device_ms (optional) = the kernel time. */
+int GhostmFormatQueriesGpu(const uint8_t *raw, uint64_t raw_len, const uint64_t *offsets,
+                           const uint32_t *lengths, uint32_t n, uint32_t width, uint32_t dna_len,
+                           uint8_t *records, int device, float *device_ms);
+
 /* One resolved hit, the record gathered across ranks (32 bytes). Coordinates are
  * subject-relative, as printed minus one. */
 typedef struct GhostmHit {
