@@ -41,6 +41,12 @@ constexpr int kNeg = -30000;           // score of a padding row (keeps it at 0)
 // K1b k_seed<BLOCK, CAP, GBUF>: one workgroup per query (by size class): gather
 //     the bins (one load per position), mark in-list repeats, merge-path tree in
 //     LDS (or global buffers for oversized queries), run-length emission.
+// lane l receives lane l-1's value (lane 0: 0) — DPP wave_shr:1, a VALU op with
+// no LDS round trip (the group-boundary lanes overwrite it with their own zeros)
+__device__ inline uint32_t ShiftUp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xF, 0xF, true);  // bound_ctrl: lane 0 reads 0
+}
+
 constexpr uint32_t kMaxLists = 128;
 constexpr uint32_t kOverflow = 0xFFFFFFFFu;
 constexpr uint32_t kMaxSlotCap = 256;  // slot pass: candidates per query slot
@@ -545,7 +551,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed_hash(SeedArgs a) {
 #pragma unroll
     for (uint32_t u = 0; u < kU; ++u) {
       const uint32_t j = lst[u];
-      const uint32_t pj = __shfl_up(j, 1), pp = __shfl_up(pos[u], 1);
+      const uint32_t pj = ShiftUp(j), pp = ShiftUp(pos[u]);
       uint32_t prev_pos = prv[u];
       if (lane > 0 && pj == j) prev_pos = pp;
       if (j != 0xFFFFFFFFu) {
@@ -638,7 +644,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
 #pragma unroll
     for (uint32_t u = 0; u < 4; ++u) {
       const uint32_t j = lst[u];
-      const uint32_t pj = __shfl_up(j, 1), pp = __shfl_up(pos[u], 1);
+      const uint32_t pj = ShiftUp(j), pp = ShiftUp(pos[u]);
       uint32_t prev_pos = prv[u];
       if (lane > 0 && pj == j) prev_pos = pp;
       uint32_t x = kNone;
@@ -879,11 +885,6 @@ __device__ inline uint32_t W(sh2 v) { return __builtin_bit_cast(uint32_t, v); }
 __device__ inline uint32_t W(us2 v) { return __builtin_bit_cast(uint32_t, v); }
 __device__ inline uint32_t W(hf2 v) { return __builtin_bit_cast(uint32_t, v); }
 
-// lane l receives lane l-1's value (lane 0: 0) — DPP wave_shr:1, a VALU op with
-// no LDS round trip (the group-boundary lanes overwrite it with their own zeros)
-__device__ inline uint32_t ShiftUp(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xF, 0xF, true);  // bound_ctrl: lane 0 reads 0
-}
 
 // Bitwise/packed helpers as single instructions: written in C the compiler
 // turns these mask selects into compare + v_cndmask pairs per half.
