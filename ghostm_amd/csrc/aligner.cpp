@@ -535,6 +535,39 @@ void Session::DevicePass(QueryData &q, DbData &d, const std::vector<uint32_t> &c
   pass.carry_in = carry_in;
   pass.carry_out = !final_pass;
   pass.chunk = d.chunk.id;
+  // Pipeline, per segment k: K2(k) is enqueued first; then segment k-1's
+  // selection (its K4/K3 finished before K2(k) started) is copied back on the
+  // copy stream, turned into records and handed to the formatter while K2(k)
+  // runs; then K4/K3(k) are enqueued behind K2(k) (after K2 finishes when its
+  // guard list needs re-scoring first). The GPU never waits for the host
+  // between segments.
+  struct Pending {
+    uint32_t g0 = 0, g1 = 0;
+    bool active = false, identity = false;
+  } pending;
+  auto finish_pending = [&] {
+    if (!pending.active) return;
+    pending.active = false;
+    const uint32_t g0 = pending.g0;
+    auto sel_counts = std::make_shared<std::vector<uint32_t>>();
+    auto sel_hits = std::make_shared<HostHits>();
+    const double t0 = NowSeconds();
+    dev.MergeCollect(sel_counts.get(), final_pass ? sel_hits.get() : nullptr);
+    stats_.seconds_merge += NowSeconds() - t0;
+    TraceMark("merge_done", pending.g1 - g0);
+    if (!final_pass) return;
+    dev.AppendRecords(q.dev, g0, *sel_counts, cap, q.global_base, false);
+    Part *part = NewPart();
+    const QueryData *qp = &q;
+    TraceMark("records", g0);
+    formatter_->Submit([this, qp, g0, sel_counts, sel_hits, cap, part] {
+      const double t = NowSeconds();
+      TraceMark("fmt_begin", g0);
+      FormatSelected(*qp, g0, *sel_counts, *sel_hits, cap, part);
+      stats_.seconds_output += NowSeconds() - t;
+      TraceMark("fmt_end", g0);
+    });
+  };
   for (size_t k = 0; k < cuts.size(); ++k) {
     const uint32_t g0 = cuts[k].first, g1 = cuts[k].second;
     const uint64_t c0 = segs[k].cand_begin, c1 = c0 + segs[k].n;
@@ -547,39 +580,43 @@ void Session::DevicePass(QueryData &q, DbData &d, const std::vector<uint32_t> &c
     const bool identity = c1 == c0 && carry_in && opt_.best <= 16;
     const bool work = c1 > c0 || (carry_in && !identity);
     TraceMark("seg", k);
-    if (c1 > c0) {
-      // the next segment's K2 tasks are built while this one's K2 runs
-      dev.Score(q.dev, d.dev, c0, c1 - c0, segs[k].q_first, segs[k].q_end, counts, offsets, base, gap, nullptr,
-                nullptr, k + 1 < segs.size() ? &segs[k + 1] : nullptr);
+    if (c1 > c0)
+      dev.ScoreLaunch(q.dev, d.dev, c0, c1 - c0, segs[k].q_first, segs[k].q_end, counts, offsets, base, gap,
+                      k + 1 < segs.size() ? &segs[k + 1] : nullptr);
+    finish_pending();  // segment k - 1, while K2(k) runs
+    const bool guarded = dev.ScoreGuarded();
+    if (work && !guarded) {
+      dev.MergeLaunch(q.dev, d.dev, g0, g1, c0, c1 - c0, opt_.best, tb_base, opt_.open_gap, opt_.extend_gap, pass);
+      pending = Pending{g0, g1, true, false};
     }
+    dev.ScoreFinish();
     TraceMark("score_done", c1 - c0);
+    if (work && guarded) {
+      dev.MergeLaunch(q.dev, d.dev, g0, g1, c0, c1 - c0, opt_.best, tb_base, opt_.open_gap, opt_.extend_gap, pass);
+      pending = Pending{g0, g1, true, false};
+    }
+    stats_.segments += 1;
+    if (work || !final_pass) continue;
+    // no K4 for these groups: their lists come straight from the carry (or are
+    // empty), formatted in order behind the pending segment's
+    finish_pending();
     auto sel_counts = std::make_shared<std::vector<uint32_t>>();
     auto sel_hits = std::make_shared<HostHits>();
-    const double t0 = NowSeconds();
-    if (work) {
-      dev.MergeSelect(q.dev, d.dev, g0, g1, c0, c1 - c0, opt_.best, tb_base, opt_.open_gap, opt_.extend_gap,
-                      sel_counts.get(), final_pass ? sel_hits.get() : nullptr, pass);
-    } else if (identity && final_pass) {
+    if (identity) {
       dev.CarryToHost(q.dev, g0, g1, cap, sel_counts.get(), sel_hits.get());
+      dev.AppendRecords(q.dev, g0, *sel_counts, cap, q.global_base, true);
     } else {
       sel_counts->assign(g1 - g0, 0);
     }
-    stats_.seconds_merge += NowSeconds() - t0;
-    stats_.segments += 1;
-    TraceMark("merge_done", g1 - g0);
-    if (!final_pass) continue;
-    if (work || identity) dev.AppendRecords(q.dev, g0, *sel_counts, cap, q.global_base, identity);
     Part *part = NewPart();
     const QueryData *qp = &q;
-    TraceMark("records", k);
-    formatter_->Submit([this, qp, g0, sel_counts, sel_hits, cap, part, k] {
+    formatter_->Submit([this, qp, g0, sel_counts, sel_hits, cap, part] {
       const double t = NowSeconds();
-      TraceMark("fmt_begin", k);
       FormatSelected(*qp, g0, *sel_counts, *sel_hits, cap, part);
       stats_.seconds_output += NowSeconds() - t;
-      TraceMark("fmt_end", k);
     });
   }
+  finish_pending();
 }
 
 void Session::RunQueryChunk(QueryData &q) {

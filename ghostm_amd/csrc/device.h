@@ -124,6 +124,15 @@ class DeviceModule {
              uint32_t q_end, const std::vector<uint32_t> &counts,
              const std::vector<uint64_t> &offsets, uint32_t base_search_length,
              const GapConfig &gap, uint32_t *score, uint32_t *end, const ScoreSegment *next = nullptr);
+  // Score() in two steps for the device-merge pipeline: ScoreLaunch enqueues K2
+  // and uploads `next`'s tasks (copy stream) with no host wait; ScoreFinish
+  // waits for K2 and re-scores its guard list. A guarded launch (ScoreGuarded)
+  // must be finished before anything reads its scores.
+  void ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32_t q_end,
+                   const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets,
+                   uint32_t base_search_length, const GapConfig &gap, const ScoreSegment *next);
+  bool ScoreGuarded() const;
+  void ScoreFinish();
 
   uint32_t ScorePerBlock(DevQuery *q, uint32_t base_search_length, const GapConfig &gap) const;
 
@@ -136,6 +145,13 @@ class DeviceModule {
   void MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, uint64_t cand_begin, uint64_t n, uint32_t best,
                    uint32_t tb_base, int open, int ext, std::vector<uint32_t> *counts,
                    HostHits *hits, const MergePass &pass = MergePass());
+  // MergeSelect in two steps: MergeLaunch enqueues K4/K3 behind the segment's
+  // K2 with no host wait; MergeCollect copies the selection back on the copy
+  // stream (the main stream meanwhile runs the next segment's K2). One launch
+  // may be outstanding; AppendRecords for it must precede the next MergeLaunch.
+  void MergeLaunch(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, uint64_t cand_begin, uint64_t n, uint32_t best,
+                   uint32_t tb_base, int open, int ext, const MergePass &pass);
+  void MergeCollect(std::vector<uint32_t> *counts, HostHits *hits);
   // Carried result lists of a query chunk (all groups empty), and their copy to
   // the host (counts[g], hits[g * cap + k]).
   void ResetCarry(DevQuery *q, uint32_t cap);
@@ -161,25 +177,17 @@ class DeviceModule {
                  uint32_t base_search_length, int open, int ext, uint32_t *db_start,
                  uint32_t *aln_len, uint32_t *aln_match, float *seq_id);
 
-  // resolves the launch timings and counters left pending by the no-wait paths
-  DeviceTimes &times() {
-    FlushTimes();
-    return times_;
-  }
-  void ResetTimes() {
-    FlushTimes();
-    times_ = DeviceTimes();
-  }
-  void FlushTimes();
+  DeviceTimes &times() { return times_; }
+  void ResetTimes() { times_ = DeviceTimes(); }
   void Synchronize();
 
  private:
   DeviceModule() = default;
-  void UploadNextTasks(const ScoreSegment *next, uint32_t per_block);
   // span: runs of slots whose hits may pair (a name group's slots)
   void LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, const DevDb *d, uint32_t span);
   int device_ = -1;
   void *stream_ = nullptr;
+  void *copy_stream_ = nullptr;  // D2H of selections and K2 task uploads, beside the kernels
   DeviceTimes times_;
   uint64_t records_ = 0;
   Impl *impl_ = nullptr;

@@ -107,37 +107,44 @@ struct DeviceModule::Impl {
   DevBuf records, rec_prefix;    // hit records of the run (HitRecord32)
   std::vector<uint32_t> h_rec_prefix;
   uint64_t ncand = 0;
-  // K2 work
-  DevBuf tasks, score_out, end_out, guard_list;
+  // K2 work: two task buffers (a launch reads one while the next segment's
+  // tasks are uploaded into the other), the guard re-score's tasks
+  DevBuf task_buf[2], tasks_redo, score_out, end_out, guard_list;
+  int task_turn = 0;
+  struct Prepared {
+    bool valid = false;
+    uint64_t cand_begin = 0, n = 0;
+    uint32_t count = 0, per_block = 0;
+    int buf = 0;
+  } prepared;
+  std::vector<kern::ScoreTask> next_tasks;  // host copy of the prepared tasks
+  struct ScoreState {                       // the launched, not yet finished K2
+    bool active = false, guarded = false;
+    uint64_t cand_begin = 0, n = 0;
+    size_t lds = 0;
+    int S = 32;
+    kern::ScoreArgs args{};
+  } score_state;
   // K3 work (tb_sort: two histograms + total, two cursor arrays)
   DevBuf tb_qid, tb_end, tb_start, tb_ml;
   DevBuf tb_width, tb_ncols, tb_key, tb_order1, tb_order2, tb_sort, tb_pair_a, tb_pair_b, tb_best;
   int cus = 256;
   // K4 work
   DevBuf keys, sel_count, sel_cand, sel_sid, slot_hits, sel_from;
+  struct MergeState {  // the launched, not yet collected K4/K3
+    bool active = false;
+    uint32_t ng = 0;
+    size_t slots = 0;
+  } merge_state;
   // result lists carried across batches / DB chunks (per group of the query
   // chunk: carry_count[g] SlotHits at carry_hits[g * cap]); DB chunk bases
   DevBuf carry_hits, carry_count, chunk_base;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  DevBuf counters;  // u64 [0] score cells, [1] traceback cells, [2] K3a scan cells
-  // K2 tasks of the next segment, built while the current one runs
-  struct Prepared {
-    uint64_t cand_begin, n, off;
-    uint32_t count, per_block;
-  };
-  DevBuf tasks_all;
-  std::vector<Prepared> prepared;
-  std::vector<kern::ScoreTask> next_tasks;  // host copy, alive until the next upload
-  // launch timings resolved after the run (no host wait per launch)
-  struct Pending {
-    hipEvent_t a, b;
-    double *dst;
-  };
-  std::vector<hipEvent_t> ev_pool;
-  size_t ev_used = 0;
-  std::vector<Pending> pending;
-  DevBuf acc;        // u64 [0]: K2 cells of deferred launches
-  bool acc_zeroed = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;          // K1 / K2 launch
+  hipEvent_t ev_m0 = nullptr, ev_m1 = nullptr;      // K4
+  hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;      // K3
+  hipEvent_t ev_done = nullptr, ev_tasks = nullptr; // end of a segment's selection; next tasks uploaded
+  DevBuf counters;     // K2: u64 [0] score cells, u32 at [2] guard count
+  DevBuf tb_counters;  // K3: u64 [0] traceback cells, [1] K3a scan cells
   bool matrix_set = false;
 };
 
@@ -194,11 +201,14 @@ void DeviceModule::Bind(int device) {
   if (device < 0 || device >= n) throw Error("device id " + std::to_string(device) + " out of range");
   HIP_CHECK(hipSetDevice(device));
   if (!impl_) impl_ = new Impl();
-  hipStream_t s;
+  hipStream_t s, c;
   HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  HIP_CHECK(hipStreamCreateWithFlags(&c, hipStreamNonBlocking));
   stream_ = s;
-  HIP_CHECK(hipEventCreate(&impl_->ev0));
-  HIP_CHECK(hipEventCreate(&impl_->ev1));
+  copy_stream_ = c;
+  for (hipEvent_t *e : {&impl_->ev0, &impl_->ev1, &impl_->ev_m0, &impl_->ev_m1, &impl_->ev_t0, &impl_->ev_t1,
+                        &impl_->ev_done, &impl_->ev_tasks})
+    HIP_CHECK(hipEventCreate(e));
   HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_seed<1024, 16384, false>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 16384 * 4));
   HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_seed<512, 8192, false>,
@@ -365,6 +375,7 @@ void DeviceModule::SetDbSubjects(DevDb *d, const uint32_t *starts, uint32_t nsub
 
 void DeviceModule::Synchronize() {
   if (stream_) HIP_CHECK(hipStreamSynchronize(S(stream_)));
+  if (copy_stream_) HIP_CHECK(hipStreamSynchronize(S(copy_stream_)));
 }
 
 static float ElapsedMs(hipEvent_t a, hipEvent_t b) {
@@ -705,51 +716,21 @@ uint32_t DeviceModule::ScorePerBlock(DevQuery *q, uint32_t base, const GapConfig
   return (kern::kScoreBlock / 64) * lay.gpw * (ScorePacked(impl_->h_matrix, q->L, base, gap) ? 2 : 1);
 }
 
-static unsigned long long *AccCells(DeviceModule::Impl &I, hipStream_t st) {
-  I.acc.Reserve(16);
-  if (!I.acc_zeroed) {
-    HIP_CHECK(hipMemsetAsync(I.acc.p, 0, 16, st));
-    I.acc_zeroed = true;
-  }
-  return I.acc.as<unsigned long long>();
-}
-
-static void NewEventPair(DeviceModule::Impl &I, hipEvent_t *a, hipEvent_t *b) {
-  while (I.ev_pool.size() < I.ev_used + 2) {
-    hipEvent_t e;
-    HIP_CHECK(hipEventCreate(&e));
-    I.ev_pool.push_back(e);
-  }
-  *a = I.ev_pool[I.ev_used++];
-  *b = I.ev_pool[I.ev_used++];
-}
-
-void DeviceModule::FlushTimes() {
-  if (!impl_) return;
-  Impl &I = *impl_;
-  if (I.pending.empty() && !I.acc_zeroed) return;
-  HIP_CHECK(hipStreamSynchronize(S(stream_)));
-  for (const Impl::Pending &p : I.pending) *p.dst += ElapsedMs(p.a, p.b) * 1e-3;
-  I.pending.clear();
-  I.ev_used = 0;
-  if (I.acc_zeroed) {
-    unsigned long long v[2] = {0, 0};
-    HIP_CHECK(hipMemcpy(v, I.acc.p, 16, hipMemcpyDeviceToHost));
-    times_.score_cells += v[0];
-    I.acc_zeroed = false;
-  }
-}
-
-void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n, uint32_t q_first,
-                         uint32_t q_end, const std::vector<uint32_t> &counts,
-                         const std::vector<uint64_t> &offsets, uint32_t base,
-                         const GapConfig &gap, uint32_t *score, uint32_t *end, const ScoreSegment *next) {
+// K2 in two steps for the device-merge pipeline: ScoreLaunch enqueues the
+// launch (no host wait) and prepares the next segment's tasks; ScoreFinish
+// waits for it, reads its counters on the copy stream (the main stream may
+// already hold the segment's K4/K3) and re-scores the guard list.
+void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n, uint32_t q_first,
+                               uint32_t q_end, const std::vector<uint32_t> &counts,
+                               const std::vector<uint64_t> &offsets, uint32_t base, const GapConfig &gap,
+                               const ScoreSegment *next) {
   Use();
   Impl &I = *impl_;
+  Impl::ScoreState &P = I.score_state;
+  P = Impl::ScoreState();
   if (n == 0) return;
   if (gap.ext > 0) throw Error("positive gap extension score is not supported");
   const Layout lay = ChooseLayout(q->L, base);
-  // packed int16 path (two candidates per lane) whenever every value fits
   int max_abs = 0;
   for (int v : I.h_matrix) max_abs = std::max(max_abs, v < 0 ? -v : v);
   // encoding: f16 pairs when every score fits the exact-integer range of f16,
@@ -770,24 +751,28 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
   int guard = framed ? (bound + sigma_max < 2040 ? 0 : (int)(2040 - sigma_max)) : (bound < 2048 ? 0 : 2000);
   if (half && getenv("GHOSTM_K2_GUARD")) guard = atoi(getenv("GHOSTM_K2_GUARD"));  // tests: force re-scores
   const uint32_t per_block = ScorePerBlock(q, base, gap);
-  // tasks: prepared for this range by the previous Score() call, else built
-  // and uploaded here
-  const kern::ScoreTask *dtasks = nullptr;
+  // tasks: prepared for this range by the previous launch (uploaded on the copy
+  // stream into the other task buffer), else built and uploaded here
+  int buf = -1;
   size_t ntasks = 0;
-  for (const auto &p : I.prepared)
-    if (p.cand_begin == cand_begin && p.n == n && p.per_block == per_block) {
-      dtasks = I.tasks_all.as<kern::ScoreTask>() + p.off;
-      ntasks = p.count;
-    }
-  if (!dtasks) {
+  if (I.prepared.valid && I.prepared.cand_begin == cand_begin && I.prepared.n == n &&
+      I.prepared.per_block == per_block) {
+    buf = I.prepared.buf;
+    ntasks = I.prepared.count;
+    HIP_CHECK(hipStreamWaitEvent(S(stream_), I.ev_tasks, 0));
+  }
+  I.prepared.valid = false;
+  if (buf < 0) {
     std::vector<kern::ScoreTask> tasks;
     BuildScoreTasks(cand_begin, n, q_first, q_end, counts, offsets, per_block, &tasks);
-    I.tasks.Reserve(tasks.size() * sizeof(kern::ScoreTask));
-    HIP_CHECK(hipMemcpyAsync(I.tasks.p, tasks.data(), tasks.size() * sizeof(kern::ScoreTask),
+    buf = I.task_turn;
+    I.task_buf[buf].Reserve(tasks.size() * sizeof(kern::ScoreTask));
+    HIP_CHECK(hipMemcpyAsync(I.task_buf[buf].p, tasks.data(), tasks.size() * sizeof(kern::ScoreTask),
                              hipMemcpyHostToDevice, S(stream_)));
-    dtasks = I.tasks.as<kern::ScoreTask>();
+    HIP_CHECK(hipStreamSynchronize(S(stream_)));  // the host vector goes out of scope
     ntasks = tasks.size();
   }
+  I.task_turn = 1 - buf;
   I.score_out.Reserve(n * 4);
   I.end_out.Reserve(n * 4);
   kern::ScoreArgs a{};
@@ -802,7 +787,7 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
   a.mat = I.mat_k2.as<int>();
   a.cand_qid = I.cand_qid.as<uint32_t>();
   a.cand_start = I.cand_start.as<uint32_t>();
-  a.tasks = dtasks;
+  a.tasks = I.task_buf[buf].as<kern::ScoreTask>();
   a.base = base;
   a.extend = gap.extend;
   a.open = gap.open;
@@ -810,28 +795,19 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
   a.score_out = I.score_out.as<uint32_t>();
   a.end_out = I.end_out.as<uint32_t>();
   a.out_base = cand_begin;
-  // nothing read back (device merge, no guard): no host wait after K2; the
-  // cell count accumulates on the device and the launch time is resolved later
-  // (off by default: measured slower on the box, 476 -> 570 ms/step, with the
-  // host waiting once per segment instead of after K2; GHOSTM_K2_NOWAIT=1 enables)
-  const char *nw = getenv("GHOSTM_K2_NOWAIT");
-  const bool nowait = nw && !strcmp(nw, "1");
-  const bool deferred = nowait && !score && !end && !(half && guard);
+  // counters: [0] cells (u64), [2] guard count (u32)
   I.counters.Reserve(32);
-  if (!deferred) HIP_CHECK(hipMemsetAsync(I.counters.p, 0, 32, S(stream_)));
-  a.cells = deferred ? AccCells(I, S(stream_)) : I.counters.as<unsigned long long>();
-  uint32_t *guard_count = reinterpret_cast<uint32_t *>(I.counters.as<unsigned long long>() + 2);
+  HIP_CHECK(hipMemsetAsync(I.counters.p, 0, 32, S(stream_)));
+  a.cells = I.counters.as<unsigned long long>();
   if (half && guard) {
     I.guard_list.Reserve((size_t)n * 8);
     a.guard = guard;
-    a.guard_count = guard_count;
+    a.guard_count = reinterpret_cast<uint32_t *>(I.counters.as<unsigned long long>() + 2);
     a.guard_list = I.guard_list.as<uint32_t>();
   }
   const size_t lds = packed ? (size_t)kern::kScoreQmax * kern::kProfRows16 * (lay.Lpad + 8) * 2
                             : (size_t)kern::kScoreQmax * kern::kProfRows * (lay.Lpad + 4) * 4;
-  hipEvent_t e0 = I.ev0, e1 = I.ev1;
-  if (deferred) NewEventPair(I, &e0, &e1);
-  HIP_CHECK(hipEventRecord(e0, S(stream_)));
+  HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
   const dim3 grid((uint32_t)ntasks), block(kern::kScoreBlock);
   if (packed) {
     switch (lay.S) {
@@ -859,67 +835,90 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
     }
   }
   HIP_CHECK(hipGetLastError());
-  HIP_CHECK(hipEventRecord(e1, S(stream_)));
+  HIP_CHECK(hipEventRecord(I.ev1, S(stream_)));
   times_.score_launches += 1;
   times_.score_launches_packed += packed ? 1 : 0;
   times_.score_launches_half += half ? 1 : 0;
   times_.score_launches_framed += framed ? 1 : 0;
-  // the next segment's tasks, built on the host while K2 runs
-  I.prepared.clear();
-  I.next_tasks.clear();
-  if (next && next->n) BuildScoreTasks(next->cand_begin, next->n, next->q_first, next->q_end, counts, offsets,
-                                       per_block, &I.next_tasks);
-  if (deferred) {
-    I.pending.push_back({e0, e1, &times_.score});
-    UploadNextTasks(next, per_block);  // stream-ordered after this K2
-    return;
+  P.active = true;
+  P.guarded = half && guard;
+  P.cand_begin = cand_begin;
+  P.n = n;
+  P.lds = lds;
+  P.S = lay.S;
+  P.args = a;
+  // the next segment's tasks, built on the host while K2 runs and uploaded on
+  // the copy stream into the other buffer (its last reader, the previous K2,
+  // has finished: ScoreFinish waited for it)
+  if (next && next->n) {
+    std::vector<kern::ScoreTask> &nt = I.next_tasks;
+    nt.clear();
+    BuildScoreTasks(next->cand_begin, next->n, next->q_first, next->q_end, counts, offsets, per_block, &nt);
+    const int nb = I.task_turn;
+    I.task_buf[nb].Reserve(nt.size() * sizeof(kern::ScoreTask));
+    HIP_CHECK(hipMemcpyAsync(I.task_buf[nb].p, nt.data(), nt.size() * sizeof(kern::ScoreTask),
+                             hipMemcpyHostToDevice, S(copy_stream_)));
+    HIP_CHECK(hipEventRecord(I.ev_tasks, S(copy_stream_)));
+    I.prepared = Impl::Prepared{true, next->cand_begin, next->n, (uint32_t)nt.size(), per_block, nb};
   }
-  if (score) HIP_CHECK(hipMemcpyAsync(score, I.score_out.p, n * 4, hipMemcpyDeviceToHost, S(stream_)));
-  if (end) HIP_CHECK(hipMemcpyAsync(end, I.end_out.p, n * 4, hipMemcpyDeviceToHost, S(stream_)));
+}
+
+bool DeviceModule::ScoreGuarded() const { return impl_ && impl_->score_state.active && impl_->score_state.guarded; }
+
+void DeviceModule::ScoreFinish() {
+  Use();
+  Impl &I = *impl_;
+  Impl::ScoreState &P = I.score_state;
+  if (!P.active) return;
+  P.active = false;
+  // the counters on the copy stream: the main stream may already hold K4/K3
   unsigned long long cells = 0;
   uint32_t nguard = 0;
-  HIP_CHECK(hipMemcpyAsync(&cells, I.counters.p, 8, hipMemcpyDeviceToHost, S(stream_)));
-  HIP_CHECK(hipMemcpyAsync(&nguard, guard_count, 4, hipMemcpyDeviceToHost, S(stream_)));
-  HIP_CHECK(hipStreamSynchronize(S(stream_)));
+  HIP_CHECK(hipStreamWaitEvent(S(copy_stream_), I.ev1, 0));
+  HIP_CHECK(hipMemcpyAsync(&cells, I.counters.p, 8, hipMemcpyDeviceToHost, S(copy_stream_)));
+  HIP_CHECK(hipMemcpyAsync(&nguard, I.counters.as<unsigned long long>() + 2, 4, hipMemcpyDeviceToHost,
+                           S(copy_stream_)));
+  HIP_CHECK(hipStreamSynchronize(S(copy_stream_)));
   times_.score += ElapsedMs(I.ev0, I.ev1) * 1e-3;
-  if (half && guard && nguard) {
+  times_.score_cells += cells;
+  if (P.guarded && nguard) {
     // exact re-score of the guarded candidates with the int16 kernel, one
-    // candidate per work item
+    // candidate per work item (nothing of this segment is queued behind K2:
+    // the pipeline waits for ScoreFinish when the launch is guarded)
     std::vector<uint32_t> list((size_t)nguard * 2);
     HIP_CHECK(hipMemcpy(list.data(), I.guard_list.p, list.size() * 4, hipMemcpyDeviceToHost));
     std::vector<kern::ScoreTask> redo(nguard);
     for (uint32_t k = 0; k < nguard; ++k)
-      redo[k] = kern::ScoreTask{cand_begin + list[2 * k], 1u, list[2 * k + 1], 1u, 0u};
-    I.tasks.Reserve(redo.size() * sizeof(kern::ScoreTask));
-    HIP_CHECK(hipMemcpy(I.tasks.p, redo.data(), redo.size() * sizeof(kern::ScoreTask), hipMemcpyHostToDevice));
-    kern::ScoreArgs r = a;
-    r.tasks = I.tasks.as<kern::ScoreTask>();
+      redo[k] = kern::ScoreTask{P.cand_begin + list[2 * k], 1u, list[2 * k + 1], 1u, 0u};
+    I.tasks_redo.Reserve(redo.size() * sizeof(kern::ScoreTask));
+    HIP_CHECK(hipMemcpy(I.tasks_redo.p, redo.data(), redo.size() * sizeof(kern::ScoreTask), hipMemcpyHostToDevice));
+    kern::ScoreArgs r = P.args;
+    r.tasks = I.tasks_redo.as<kern::ScoreTask>();
     r.guard = 0;
     r.cells = I.counters.as<unsigned long long>() + 3;  // not counted twice
-    const dim3 rgrid(nguard);
-    switch (lay.S) {
-      case 32: hipLaunchKernelGGL((kern::k_score16<32, false>), rgrid, block, lds, S(stream_), r); break;
-      case 16: hipLaunchKernelGGL((kern::k_score16<16, false>), rgrid, block, lds, S(stream_), r); break;
-      default: hipLaunchKernelGGL((kern::k_score16<8, false>), rgrid, block, lds, S(stream_), r); break;
+    const dim3 rgrid(nguard), block(kern::kScoreBlock);
+    switch (P.S) {
+      case 32: hipLaunchKernelGGL((kern::k_score16<32, false>), rgrid, block, P.lds, S(stream_), r); break;
+      case 16: hipLaunchKernelGGL((kern::k_score16<16, false>), rgrid, block, P.lds, S(stream_), r); break;
+      default: hipLaunchKernelGGL((kern::k_score16<8, false>), rgrid, block, P.lds, S(stream_), r); break;
     }
     HIP_CHECK(hipGetLastError());
-    if (score) HIP_CHECK(hipMemcpyAsync(score, I.score_out.p, n * 4, hipMemcpyDeviceToHost, S(stream_)));
-    if (end) HIP_CHECK(hipMemcpyAsync(end, I.end_out.p, n * 4, hipMemcpyDeviceToHost, S(stream_)));
     HIP_CHECK(hipStreamSynchronize(S(stream_)));
     times_.score_rechecks += nguard;
   }
-  times_.score_cells += cells;
-  UploadNextTasks(next, per_block);
 }
 
-// after the current K2 has finished (its tasks may live in tasks_all)
-void DeviceModule::UploadNextTasks(const ScoreSegment *next, uint32_t per_block) {
+void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n, uint32_t q_first,
+                         uint32_t q_end, const std::vector<uint32_t> &counts,
+                         const std::vector<uint64_t> &offsets, uint32_t base,
+                         const GapConfig &gap, uint32_t *score, uint32_t *end, const ScoreSegment *next) {
+  if (n == 0) return;
+  ScoreLaunch(q, d, cand_begin, n, q_first, q_end, counts, offsets, base, gap, next);
+  ScoreFinish();
   Impl &I = *impl_;
-  if (!next || I.next_tasks.empty()) return;
-  I.tasks_all.Reserve(I.next_tasks.size() * sizeof(kern::ScoreTask));
-  HIP_CHECK(hipMemcpyAsync(I.tasks_all.p, I.next_tasks.data(), I.next_tasks.size() * sizeof(kern::ScoreTask),
-                           hipMemcpyHostToDevice, S(stream_)));
-  I.prepared.push_back({next->cand_begin, next->n, 0, (uint32_t)I.next_tasks.size(), per_block});
+  if (score) HIP_CHECK(hipMemcpyAsync(score, I.score_out.p, n * 4, hipMemcpyDeviceToHost, S(stream_)));
+  if (end) HIP_CHECK(hipMemcpyAsync(end, I.end_out.p, n * 4, hipMemcpyDeviceToHost, S(stream_)));
+  if (score || end) HIP_CHECK(hipStreamSynchronize(S(stream_)));
 }
 
 // K3 launch: the key formulation when its field widths hold (len < 511,
@@ -1104,17 +1103,20 @@ void DeviceModule::CarryToHost(DevQuery *q, uint32_t g0, uint32_t g1, uint32_t c
   HIP_CHECK(hipStreamSynchronize(S(stream_)));
 }
 
-void DeviceModule::MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, uint64_t cand_begin, uint64_t n,
-                               uint32_t best, uint32_t tb_base, int open, int ext,
-                               std::vector<uint32_t> *counts, HostHits *hits,
-                               const MergePass &pass) {
+// K4 + K3 + finalize enqueued behind the segment's K2, no host wait (ev_done
+// marks the end); MergeCollect copies the selection back on the copy stream.
+void DeviceModule::MergeLaunch(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, uint64_t cand_begin, uint64_t n,
+                               uint32_t best, uint32_t tb_base, int open, int ext, const MergePass &pass) {
   Use();
   Impl &I = *impl_;
+  Impl::MergeState &P = I.merge_state;
+  if (P.active) throw Error("MergeLaunch: the previous selection was not collected");
   if (g1 > q->ngroups || g0 > g1) throw Error("group range outside the chunk");
   const uint32_t ng = g1 - g0;
   const uint32_t cap = std::max<uint32_t>(best, 1);
-  counts->assign(ng, 0);
-  if (hits) *hits = HostHits();
+  P = Impl::MergeState();
+  P.ng = ng;
+  P.slots = (size_t)ng * cap;
   if (ng == 0) return;
   if (d->nsubj == 0) throw Error("DB subjects not set for the device merge");
   const size_t slots = (size_t)ng * cap;
@@ -1157,8 +1159,7 @@ void DeviceModule::MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, 
   m.carry_count = carry_in ? I.carry_count.as<uint32_t>() + g0 : nullptr;
   m.carry = carry_in ? I.carry_hits.as<kern::SlotHit>() + (size_t)g0 * cap : nullptr;
   m.sel_from = carry_in ? I.sel_from.as<uint32_t>() : nullptr;
-  hipEvent_t m0 = I.ev0, m1 = I.ev1;
-  HIP_CHECK(hipEventRecord(m0, S(stream_)));
+  HIP_CHECK(hipEventRecord(I.ev_m0, S(stream_)));
   // K4: one wave per name group (keys in LDS) for -b up to kMergeBest, else
   // one thread per group; GHOSTM_K4=thread|wave forces one (tests)
   bool wave = best >= 1 && best <= kern::kMergeBest;
@@ -1177,8 +1178,7 @@ void DeviceModule::MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, 
   times_.merge_launches += 1;
   times_.merge_launches_wave += wave ? 1 : 0;
   HIP_CHECK(hipGetLastError());
-  HIP_CHECK(hipEventRecord(m1, S(stream_)));
-  times_.merge += ElapsedMs(m0, m1) * 1e-3;
+  HIP_CHECK(hipEventRecord(I.ev_m1, S(stream_)));
 
   // K3 over the slots (empty slots carry qid 0xFFFFFFFF and are skipped)
   kern::TbArgs a{};
@@ -1194,12 +1194,13 @@ void DeviceModule::MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, 
   a.ext = ext;
   a.out_start = I.tb_start.as<uint32_t>();
   a.out_ml = I.tb_ml.as<uint32_t>();
-  I.counters.Reserve(32);
-  HIP_CHECK(hipMemsetAsync(I.counters.p, 0, 24, S(stream_)));
-  a.cells = I.counters.as<unsigned long long>() + 1;
-  HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
+  // K3 counters: [0] traceback cells, [1] K3a scan cells
+  I.tb_counters.Reserve(16);
+  HIP_CHECK(hipMemsetAsync(I.tb_counters.p, 0, 16, S(stream_)));
+  a.cells = I.tb_counters.as<unsigned long long>();
+  HIP_CHECK(hipEventRecord(I.ev_t0, S(stream_)));
   LaunchTraceback(a, q, (uint32_t)slots, d, cap);
-  HIP_CHECK(hipEventRecord(I.ev1, S(stream_)));
+  HIP_CHECK(hipEventRecord(I.ev_t1, S(stream_)));
   hipLaunchKernelGGL(kern::k_finalize, dim3((uint32_t)((slots + 255) / 256)), dim3(256), 0, S(stream_),
                      I.sel_count.as<uint32_t>(), I.sel_cand.as<uint32_t>(), I.sel_sid.as<uint32_t>(),
                      I.score_out.as<uint32_t>(), I.end_out.as<uint32_t>(), I.tb_start.as<uint32_t>(),
@@ -1213,21 +1214,44 @@ void DeviceModule::MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, 
     HIP_CHECK(hipMemcpyAsync(I.carry_hits.as<kern::SlotHit>() + (size_t)g0 * cap, I.slot_hits.p,
                              slots * sizeof(kern::SlotHit), hipMemcpyDeviceToDevice, S(stream_)));
   }
-  unsigned long long cells = 0;
-  HIP_CHECK(hipMemcpyAsync(counts->data(), I.sel_count.p, (size_t)ng * 4, hipMemcpyDeviceToHost, S(stream_)));
+  HIP_CHECK(hipEventRecord(I.ev_done, S(stream_)));
+  P.active = true;
+}
+
+// Waits for the launched K4/K3 and copies counts[ng] (and, unless hits is null,
+// the ng * cap selected hits) back on the copy stream, so the main stream can
+// already run the next segment's K2. The device buffers are not reused before
+// this returns: the next MergeLaunch is issued after it.
+void DeviceModule::MergeCollect(std::vector<uint32_t> *counts, HostHits *hits) {
+  Use();
+  Impl &I = *impl_;
+  Impl::MergeState &P = I.merge_state;
+  counts->assign(P.ng, 0);
+  if (hits) *hits = HostHits();
+  if (!P.active) return;
+  P.active = false;
+  unsigned long long cells[2] = {0, 0};
+  HIP_CHECK(hipStreamWaitEvent(S(copy_stream_), I.ev_done, 0));
+  HIP_CHECK(hipMemcpyAsync(counts->data(), I.sel_count.p, (size_t)P.ng * 4, hipMemcpyDeviceToHost,
+                           S(copy_stream_)));
   if (hits) {  // null: the selection stays on the device (a carried pass)
-    AcquireHostHits(slots, hits);
-    HIP_CHECK(hipMemcpyAsync(hits->data, I.slot_hits.p, slots * sizeof(SelectedHit), hipMemcpyDeviceToHost,
-                             S(stream_)));
+    AcquireHostHits(P.slots, hits);
+    HIP_CHECK(hipMemcpyAsync(hits->data, I.slot_hits.p, P.slots * sizeof(SelectedHit), hipMemcpyDeviceToHost,
+                             S(copy_stream_)));
   }
-  unsigned long long scan_cells = 0;
-  HIP_CHECK(hipMemcpyAsync(&cells, I.counters.as<unsigned long long>() + 1, 8, hipMemcpyDeviceToHost, S(stream_)));
-  HIP_CHECK(hipMemcpyAsync(&scan_cells, I.counters.as<unsigned long long>() + 2, 8, hipMemcpyDeviceToHost,
-                           S(stream_)));
-  HIP_CHECK(hipStreamSynchronize(S(stream_)));
-  times_.traceback += ElapsedMs(I.ev0, I.ev1) * 1e-3;
-  times_.traceback_cells += cells;
-  times_.traceback_scan_cells += scan_cells;
+  HIP_CHECK(hipMemcpyAsync(cells, I.tb_counters.p, 16, hipMemcpyDeviceToHost, S(copy_stream_)));
+  HIP_CHECK(hipStreamSynchronize(S(copy_stream_)));
+  times_.merge += ElapsedMs(I.ev_m0, I.ev_m1) * 1e-3;
+  times_.traceback += ElapsedMs(I.ev_t0, I.ev_t1) * 1e-3;
+  times_.traceback_cells += cells[0];
+  times_.traceback_scan_cells += cells[1];
+}
+
+void DeviceModule::MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, uint64_t cand_begin, uint64_t n,
+                               uint32_t best, uint32_t tb_base, int open, int ext, std::vector<uint32_t> *counts,
+                               HostHits *hits, const MergePass &pass) {
+  MergeLaunch(q, d, g0, g1, cand_begin, n, best, tb_base, open, ext, pass);
+  MergeCollect(counts, hits);
 }
 
 void DeviceModule::ResetRecords() { records_ = 0; }
@@ -1320,9 +1344,9 @@ void DeviceModule::TraceBack(DevQuery *q, DevDb *d, uint32_t n, const uint32_t *
   a.ext = ext;
   a.out_start = I.tb_start.as<uint32_t>();
   a.out_ml = I.tb_ml.as<uint32_t>();
-  I.counters.Reserve(32);
-  HIP_CHECK(hipMemsetAsync(I.counters.p, 0, 24, S(stream_)));
-  a.cells = I.counters.as<unsigned long long>() + 1;
+  I.tb_counters.Reserve(16);
+  HIP_CHECK(hipMemsetAsync(I.tb_counters.p, 0, 16, S(stream_)));
+  a.cells = I.tb_counters.as<unsigned long long>();
   HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
   LaunchTraceback(a, q, n, d, kern::kPairRun);
   HIP_CHECK(hipEventRecord(I.ev1, S(stream_)));
@@ -1331,8 +1355,8 @@ void DeviceModule::TraceBack(DevQuery *q, DevDb *d, uint32_t n, const uint32_t *
   HIP_CHECK(hipMemcpyAsync(ml.data(), I.tb_ml.p, (size_t)n * 4, hipMemcpyDeviceToHost, S(stream_)));
   unsigned long long cells = 0;
   unsigned long long scan_cells = 0;
-  HIP_CHECK(hipMemcpyAsync(&cells, I.counters.as<unsigned long long>() + 1, 8, hipMemcpyDeviceToHost, S(stream_)));
-  HIP_CHECK(hipMemcpyAsync(&scan_cells, I.counters.as<unsigned long long>() + 2, 8, hipMemcpyDeviceToHost,
+  HIP_CHECK(hipMemcpyAsync(&cells, I.tb_counters.p, 8, hipMemcpyDeviceToHost, S(stream_)));
+  HIP_CHECK(hipMemcpyAsync(&scan_cells, I.tb_counters.as<unsigned long long>() + 1, 8, hipMemcpyDeviceToHost,
                            S(stream_)));
   HIP_CHECK(hipStreamSynchronize(S(stream_)));
   times_.traceback += ElapsedMs(I.ev0, I.ev1) * 1e-3;
