@@ -1,7 +1,9 @@
 // aligner.cpp — see aligner.h.
 #include "aligner.h"
 
+#include <fcntl.h>
 #include <getopt.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -257,10 +259,14 @@ void Session::ApplyShard(uint32_t rank, uint32_t world) {
 Session::Session(const AlignerOptions &opt, uint32_t shard_rank, uint32_t shard_world) : opt_(opt) {
   threads_ = HostThreads();
   DeviceModule &dev = DeviceModule::Get();
+  TraceMark("create");
   dev.Bind(opt_.device);
+  TraceMark("bound");
   dev.SetMatrix(opt_.matrix.m.data());
 
-  // query chunks: -S start (or 0) .. -L end, as Execute walks them (aligner.cpp:98-204)
+  // query chunks: -S start (or 0) .. -L end, as Execute walks them
+  // (aligner.cpp:98-204), and every DB chunk; the chunk files are read on
+  // parallel threads, then the chunks up to the first missing one are kept
   QueryFile qf(opt_.query_prefix);
   uint32_t id = opt_.start_query_chunk == UINT32_MAX ? 0 : opt_.start_query_chunk;
   uint32_t base = 0;
@@ -270,30 +276,43 @@ Session::Session(const AlignerOptions &opt, uint32_t shard_rank, uint32_t shard_
     if (f) f.read(reinterpret_cast<char *>(&n), 4);
     base += n;
   }
-  for (;;) {
-    QueryData qd;
-    if (!qf.ReadChunk(id, &qd.chunk)) break;
-    qd.global_base = base;
-    base += qd.chunk.nseq;
-    queries_.push_back(std::move(qd));
-    ++id;
-    if (!(id <= opt_.end_query_chunk)) break;
+  // chunk `id`, then the following ones up to -L (at least `id` itself)
+  uint32_t nq_chunks = 0;
+  if ((int64_t)id < (int64_t)qf.division) {
+    const uint64_t last = std::min<uint64_t>(opt_.end_query_chunk, (uint64_t)qf.division - 1);
+    nq_chunks = (uint32_t)(last >= id ? last - id + 1 : 1);
+  }
+  DbFile df(opt_.db_prefix);
+  const uint32_t nd_chunks = (int64_t)df.division > 0 ? (uint32_t)df.division : 0u;
+  std::vector<QueryData> qread(nq_chunks);
+  std::vector<DbData> dread(nd_chunks);
+  std::vector<char> qok(nq_chunks, 0), dok(nd_chunks, 0);
+  ParallelFor(nq_chunks + nd_chunks, std::max<unsigned>(1u, std::min(threads_, 8u)),
+              [&](size_t b, size_t e, unsigned) {
+                for (size_t k = b; k < e; ++k) {
+                  if (k < nq_chunks) qok[k] = qf.ReadChunk(id + (uint32_t)k, &qread[k].chunk);
+                  else dok[k - nq_chunks] = df.ReadChunk((uint32_t)(k - nq_chunks), &dread[k - nq_chunks].chunk);
+                }
+              });
+  for (uint32_t k = 0; k < nq_chunks && qok[k]; ++k) {
+    qread[k].global_base = base;
+    base += qread[k].chunk.nseq;
+    queries_.push_back(std::move(qread[k]));
   }
   if (queries_.empty()) throw std::runtime_error("[Aligner] error: don't find query file.");
+  TraceMark("queries_read", queries_.size());
   if (shard_world == 0 || shard_rank >= shard_world) throw std::invalid_argument("shard rank outside the world");
   if (shard_world > 1) ApplyShard(shard_rank, shard_world);  // may leave no queries
 
-  DbFile df(opt_.db_prefix);
   db_sum_u32_ = (uint32_t)df.sum_length;
   uint32_t dbase = 0;
-  for (uint32_t k = 0;; ++k) {
-    DbData dd;
-    if (!df.ReadChunk(k, &dd.chunk)) break;
-    dd.global_base = dbase;
-    dbase += dd.chunk.nseq;
-    dbs_.push_back(std::move(dd));
+  for (uint32_t k = 0; k < nd_chunks && dok[k]; ++k) {
+    dread[k].global_base = dbase;
+    dbase += dread[k].chunk.nseq;
+    dbs_.push_back(std::move(dread[k]));
   }
   if (dbs_.empty()) throw std::runtime_error("[Aligner] error: don't find db file.");
+  TraceMark("db_read", dbs_.size());
 
   for (QueryData &q : queries_) {
     const uint32_t n = q.chunk.nseq, L = q.chunk.L;
@@ -324,6 +343,7 @@ Session::Session(const AlignerOptions &opt, uint32_t shard_rank, uint32_t shard_
     dev.SetChunkBases(bases.data(), (uint32_t)bases.size());
   }
   dev.Synchronize();
+  TraceMark("uploaded");
   formatter_.reset(new TaskQueue());
 }
 
@@ -1045,9 +1065,48 @@ size_t Session::DeviceHits(void *dst, size_t cap) {
 }
 
 void Session::WriteOutputFile() {
-  std::ofstream out(opt_.output_file.c_str(), std::ios::binary);
+  TraceMark("write");
+  struct Done {
+    ~Done() {
+      TraceMark("written");
+      TraceDump();
+    }
+  } done;
+  // the pieces in output order, written at their offsets by parallel threads
+  // (an unwritable path writes nothing, as the reference's unchecked ofstream)
+  std::vector<const std::string *> pieces;
+  std::vector<uint64_t> at;
+  uint64_t total = 0;
   for (size_t k = 0; k < used_parts_; ++k)
-    for (const std::string &t : parts_[k].text) out.write(t.data(), (std::streamsize)t.size());
+    for (const std::string &t : parts_[k].text) {
+      if (t.empty()) continue;
+      pieces.push_back(&t);
+      at.push_back(total);
+      total += t.size();
+    }
+  const int fd = open(opt_.output_file.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+  if (fd < 0) return;
+  std::vector<char> failed(pieces.size(), 0);
+  ParallelFor(pieces.size(), std::max<unsigned>(1u, std::min(threads_, 8u)), [&](size_t b, size_t e, unsigned) {
+    for (size_t k = b; k < e; ++k) {
+      const char *p = pieces[k]->data();
+      size_t left = pieces[k]->size();
+      off_t off = (off_t)at[k];
+      while (left) {
+        const ssize_t w = pwrite(fd, p, left, off);
+        if (w <= 0) {
+          failed[k] = 1;
+          break;
+        }
+        p += w;
+        off += w;
+        left -= (size_t)w;
+      }
+    }
+  });
+  close(fd);
+  for (char f : failed)
+    if (f) throw Error("writing " + opt_.output_file + " failed");
 }
 
 // defined after LineFormat (a complete type for format_)
