@@ -189,7 +189,21 @@ AlignerOptions ParseAlignerOptions(int argc, char **argv) {
   // small inputs); the oracle honours the same variable
   if (const char *e = getenv("GHOSTM_MAX_LIST_OVERRIDE")) o.max_list_length = (uint32_t)strtoul(e, nullptr, 10);
   o.matrix = ReadScoreMatrix(matrix_file);
-  if (o.output_style == 0) o.karlin = GappedKarlinParams(o.matrix, o.open_gap, o.extend_gap);
+  if (o.output_style == 0) {
+    // extension: GHOSTM_KARLIN=ungapped prices combinations the
+    // reference's table lacks with the matrix's ungapped ideal parameters
+    // (karlin_params.cpp); unset, they throw as the reference does
+    const char *kp = getenv("GHOSTM_KARLIN");
+    if (kp && std::string(kp) == "ungapped") {
+      try {
+        o.karlin = GappedKarlinParams(o.matrix, o.open_gap, o.extend_gap);
+      } catch (std::invalid_argument &) {
+        o.karlin = UngappedKarlinParams(o.matrix);
+      }
+    } else {
+      o.karlin = GappedKarlinParams(o.matrix, o.open_gap, o.extend_gap);
+    }
+  }
   return o;
 }
 

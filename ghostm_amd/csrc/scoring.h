@@ -32,6 +32,14 @@ struct KarlinParams {
 // combination throws "error: not support score option".
 KarlinParams GappedKarlinParams(const ScoreMatrix &mx, int open_gap, int extend_gap);
 
+// General ungapped parameters for any matrix (karlin_params.cpp): the reference's
+// Statistics::CalculateUngappedIdealKarlinParameters (statistics.cpp:100-112) with
+// BLAST's routines (karlin.cpp:16-324), Robinson & Robinson background.
+KarlinParams UngappedKarlinParams(const ScoreMatrix &mx);
+// BlastComputeLengthAdjustment (karlin.cpp:393-476); returns 0 when converged.
+int LengthAdjustment(float K, float logK, float alpha_d_lambda, float beta, int query_length, uint32_t db_length,
+                     int db_num_seqs, int *adjustment);
+
 // Float/double arithmetic exactly as the reference (A.7 of SURVEY.md):
 //   bits = ((float)s * lambda - logf(K)) / (float)log(2.0)
 //   E    = (float)((double)((float)space * K) * exp(-1.0 * s * (double)lambda))

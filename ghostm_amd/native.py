@@ -104,6 +104,9 @@ SIGNATURES = {
                                     POINTER(c_float)]),
     "GhostmFormatQueriesGpu": (c_int, [POINTER(ctypes.c_uint8), c_uint64, POINTER(c_uint64), u32p, c_uint32, c_uint32,
                                        c_uint32, POINTER(ctypes.c_uint8), c_int, POINTER(c_float)]),
+    "GhostmKarlinUngapped": (c_int, [POINTER(c_int), POINTER(c_float), POINTER(c_float), POINTER(c_float)]),
+    "GhostmReadScoreMatrix": (c_int, [c_char_p, POINTER(c_int)]),
+    "GhostmLengthAdjustment": (c_int, [c_float, c_float, c_float, c_float, c_int, c_uint32, c_int, POINTER(c_int)]),
     "GhostmSessionCreate": (c_void_p, [c_int, POINTER(c_char_p)]),
     "GhostmSessionCreateShard": (c_void_p, [c_int, POINTER(c_char_p), c_int, c_int]),
     "GhostmSessionShardRange": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),

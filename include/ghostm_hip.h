@@ -130,6 +130,27 @@ int GhostmFormatQueriesGpu(const uint8_t *raw, uint64_t raw_len, const uint64_t 
                            const uint32_t *lengths, uint32_t n, uint32_t width, uint32_t dna_len,
                            uint8_t *records, int device, float *device_ms);
 
+/* General Karlin-Altschul parameters. The reference `aln` knows
+ * only two gapped parameter sets (statistics.cpp:134-146); its vendored routines
+ * compute ungapped ones for any matrix. GhostmKarlinUngapped restates
+ * Statistics::CalculateUngappedIdealKarlinParameters (statistics.cpp:100-112,
+ * Robinson & Robinson background) with BlastKarlinBlkCalc (karlin.cpp:16-32) on
+ * a 32x32 matrix M[db_code*32 + query_code]; the floats are bit-identical to the
+ * reference's. `aln` uses them for E-values of matrix/gap combinations outside
+ * the table when GHOSTM_KARLIN=ungapped is set (otherwise the reference's error). */
+int GhostmKarlinUngapped(const int score_matrix[], float *lambda, float *K, float *H);
+
+/* The 32x32 matrix `aln -M path` scores with (ScoreMatrixReader::Read,
+ * score_matrix_reader.cpp:44-113: built-in BLOSUM62 when the path cannot be
+ * opened), row-major M[db_code*32 + query_code]; the input GhostmKarlinUngapped takes. */
+int GhostmReadScoreMatrix(const char *path, int score_matrix[]);
+
+/* BlastComputeLengthAdjustment (karlin.cpp:393-476): the edge-effect length
+ * adjustment; returns 0 when the iteration converged, 1 otherwise, as the
+ * reference. */
+int GhostmLengthAdjustment(float K, float logK, float alpha_d_lambda, float beta, int query_length,
+                           uint32_t db_length, int db_num_seqs, int *length_adjustment);
+
 /* One resolved hit, the record gathered across ranks (32 bytes). Coordinates are
  * subject-relative, as printed minus one. */
 typedef struct GhostmHit {

@@ -350,3 +350,28 @@ def test_merge_modes_match_golden(mode, ds, var, opts, dataset, golden, tmp_path
     assert cases.sha256(str(tmp_path / "g.out")) == golden["aln"][f"{ds}/{var}"]["sha256"]
     assert st["merge_launches"] > 0
     assert st["merge_launches_wave"] == (0 if mode == "thread" else st["merge_launches"])
+
+
+def test_gpu_ungapped_karlin_evalues(dataset, tmp_path):
+    """§8 f4: PAM250 with -y 0 is outside the reference's gapped table and raises
+    there (statistics.cpp:143-145); GHOSTM_KARLIN=ungapped prices it with the
+    matrix's ungapped ideal parameters (bit-pinned in test_karlin.py). The bits
+    column must be ((float)s * lambda - logf(K)) / (float)log(2) of the score -y 1
+    prints for the same hit (statistics.cpp:40-44)."""
+    from ghostm_amd import statistics
+    d = dataset("syn_small")
+    opts = ["-M", cases.PAM250]
+    with pytest.raises(Exception):
+        _gpu_text(d, opts + ["-y", "0"], {}, str(tmp_path / "a.out"))
+    t0, _ = _gpu_text(d, opts + ["-y", "0"], {"GHOSTM_KARLIN": "ungapped"}, str(tmp_path / "b.out"))
+    t1, _ = _gpu_text(d, opts + ["-y", "1"], {}, str(tmp_path / "c.out"))
+    l0, l1 = t0.decode().splitlines(), t1.decode().splitlines()
+    assert len(l0) == len(l1) > 0
+    p = statistics.ungapped_ideal_karlin(cases.PAM250)
+    lam, logk, ln2 = np.float32(p.lambda_), np.log(np.float32(p.K)), np.float32(np.log(2.0))
+    for a, b in zip(l0, l1):
+        fa, fb = a.split("\t"), b.split("\t")
+        assert fa[:2] == fb[:2]
+        want = (np.float32(int(fb[2])) * lam - logk) / ln2
+        assert float(fa[8]) == pytest.approx(float(want), rel=1e-5)  # %g keeps 6 digits
+        assert float(fa[7]) > 0.0
