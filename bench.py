@@ -188,7 +188,9 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     dist = None
-    if world > 1:
+    # GHOSTM_BENCH_DIST=1 takes the collective path at world 1 too (under
+    # torchrun --nproc-per-node 1): RCCL init, the record gather, the reductions
+    if world > 1 or os.environ.get("GHOSTM_BENCH_DIST") == "1":
         import torch
         import torch.distributed as dist
 
@@ -196,7 +198,10 @@ def main() -> None:
         # RCCL ("nccl") over xGMI; GHOSTM_BENCH_BACKEND=gloo rehearses the same
         # calls on a one-GPU machine (RCCL refuses two ranks on one device)
         backend = os.environ.get("GHOSTM_BENCH_BACKEND", "nccl")
-        dist.init_process_group(backend)
+        if backend == "nccl":
+            dist.init_process_group(backend, device_id=torch.device("cuda", _device()))
+        else:
+            dist.init_process_group(backend)
         coll_dev = "cuda" if backend == "nccl" else "cpu"
     from ghostm_amd.aligner import HIT_DTYPE, Session
 
