@@ -2,8 +2,10 @@
 // opcode and encoding (VOP1/VOP2 4-byte, VOP3/VOP3P 8-byte, DPP, SDWA), from wall
 // time: 8 independent chains per wave, 8 waves per SIMD, 256 CUs.
 //   hipcc -O3 --offload-arch=gfx950 valu_issue.hip -o valu_issue && ./valu_issue
-// Prints G wave-instructions/s and SIMD cycles per instruction at the clock the
-// kernel's own s_memtime reports.
+// Prints G wave-instructions/s (wall time) and s_memtime ticks per instruction.
+// s_memtime does not tick at the shader clock on gfx950 (it reads ~1.4 GHz
+// where GRBM_GUI_ACTIVE shows ~2.4 GHz), so cycles per instruction come from a
+// rocprofv3 PMC pass instead: tools/valu_pmc_summary.py.
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdio>
@@ -186,7 +188,7 @@ int run(const char *name, int waves_per_simd) {
   const double per_wave = (double)kIters * InstrPerIter(OP);
   const double total = per_wave * blocks * 4;
   const double clk = avg / (ms * 1e6);  // GHz
-  printf("%-28s w=%d  %7.1f G wave-instr/s   %.2f SIMD-cycles/instr at %.2f GHz\n", name, waves_per_simd,
+  printf("%-28s w=%d  %7.1f G wave-instr/s   %.2f s_memtime ticks/instr (%.2f G ticks/s)\n", name, waves_per_simd,
          total / (ms * 1e6), avg / per_wave / waves_per_simd, clk);
   delete[] h;
   CHECK(hipFree(cyc));
