@@ -11,13 +11,18 @@
 //   k_index_keys    one thread per position j: the window test and the key
 //                   (sentinel 32^weight = no key), key counts by atomics
 //   k_scan_*        in-place inclusive scan of the counts -> keys_count
-//   radix sort      (key, j) pairs, stable LSD over 5*weight + 1 bits
-//                   (hipCUB/rocPRIM): j ascending within each key, the keyless
-//                   windows (sentinel) last, so positions = the first npos values
+//   k_rs_*          stable LSD radix sort of the (key, j) pairs, 8-bit digits
+//                   over 5*weight + 1 bits: per 4096-element tile a digit
+//                   histogram, one scan of the (digit, tile) counts, then each
+//                   tile scatters its elements in order (ranks within a wave by
+//                   ballot matching of the digit bits, across waves by an LDS
+//                   prefix). j ascending within each key, the keyless windows
+//                   (sentinel) last, so positions = the first npos values.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <string>
+#include <utility>
 
 #include "../../include/ghostm_hip.h"
 #include "common.h"
@@ -127,6 +132,90 @@ __global__ __launch_bounds__(kIdxBlock) void k_scan_add(uint32_t *x, uint32_t n,
   if (i < n) x[i] += tile_prefix[i / kScanTile];
 }
 
+// ---- stable LSD radix sort (key, value), 8-bit digits
+constexpr uint32_t kRsBits = 8, kRsDigits = 1u << kRsBits;
+constexpr uint32_t kRsWaves = 4, kRsItems = 16;                 // 256 threads, 16 elements each
+constexpr uint32_t kRsTile = 64 * kRsItems * kRsWaves;          // elements per tile (block)
+static_assert(kIdxBlock == 64 * kRsWaves && kIdxBlock == kRsDigits, "one thread per digit");
+
+// Digit counts of tile t, digit-major: hist[d * ntiles + t].
+__global__ __launch_bounds__(kIdxBlock) void k_rs_hist(const uint32_t *key, uint32_t n, uint32_t shift,
+                                                        uint32_t ntiles, uint32_t *hist) {
+  __shared__ uint32_t s_h[kRsDigits];
+  s_h[threadIdx.x] = 0;
+  __syncthreads();
+  const size_t t0 = (size_t)blockIdx.x * kRsTile;
+  for (uint32_t k = threadIdx.x; k < kRsTile; k += kIdxBlock) {
+    const size_t i = t0 + k;
+    if (i < n) atomicAdd(&s_h[(key[i] >> shift) & (kRsDigits - 1)], 1u);
+  }
+  __syncthreads();
+  hist[(size_t)threadIdx.x * ntiles + blockIdx.x] = s_h[threadIdx.x];
+}
+
+// Scatter of tile t in element order. incl = inclusive scan of hist (digit-major),
+// so the tile's first slot for digit d is incl[d * ntiles + t] - (tile's count of
+// d). Wave w owns elements [t*kRsTile + w*1024, +1024), batch u = 64 consecutive
+// ones; a lane's rank among same-digit lanes of a batch comes from the ballots of
+// the eight digit bits, the counts of earlier batches from the wave's LDS row.
+__global__ __launch_bounds__(kIdxBlock) void k_rs_scatter(const uint32_t *key_in, const uint32_t *val_in, uint32_t n,
+                                                           uint32_t shift, uint32_t ntiles, const uint32_t *incl,
+                                                           uint32_t *key_out, uint32_t *val_out, bool write_keys) {
+  __shared__ uint32_t s_cnt[kRsWaves][kRsDigits];
+  __shared__ uint32_t s_base[kRsDigits];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (uint32_t v = 0; v < kRsWaves; ++v) s_cnt[v][threadIdx.x] = 0;
+  __syncthreads();
+  const size_t first = (size_t)blockIdx.x * kRsTile + (size_t)w * (64 * kRsItems);
+  const unsigned long long lt = (1ull << lane) - 1;
+  uint32_t keys[kRsItems], vals[kRsItems], rank[kRsItems];
+#pragma unroll
+  for (uint32_t u = 0; u < kRsItems; ++u) {
+    const size_t i = first + u * 64 + lane;
+    const bool valid = i < n;
+    keys[u] = valid ? key_in[i] : 0u;
+    vals[u] = valid ? val_in[i] : 0u;
+    const uint32_t d = (keys[u] >> shift) & (kRsDigits - 1);
+    unsigned long long peers = __ballot(valid);
+#pragma unroll
+    for (uint32_t b = 0; b < kRsBits; ++b) {
+      const unsigned long long bal = __ballot((d >> b) & 1u);
+      peers &= ((d >> b) & 1u) ? bal : ~bal;
+    }
+    // all lanes read the count before the leaders (lowest lane of each digit)
+    // write it back: LDS operations of one wave complete in program order
+    const uint32_t before = valid ? s_cnt[w][d] : 0u;
+    rank[u] = before + (uint32_t)__popcll(peers & lt);
+    __builtin_amdgcn_wave_barrier();
+    if (valid && (peers & lt) == 0) s_cnt[w][d] = before + (uint32_t)__popcll(peers);
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  {  // per digit: exclusive prefix over the waves, and the tile's global base
+    const uint32_t d = threadIdx.x;
+    uint32_t pre = 0;
+#pragma unroll
+    for (uint32_t v = 0; v < kRsWaves; ++v) {
+      const uint32_t c = s_cnt[v][d];
+      s_cnt[v][d] = pre;
+      pre += c;
+    }
+    s_base[d] = incl[(size_t)d * ntiles + blockIdx.x] - pre;
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t u = 0; u < kRsItems; ++u) {
+    const size_t i = first + u * 64 + lane;
+    if (i < n) {
+      const uint32_t d = (keys[u] >> shift) & (kRsDigits - 1);
+      const uint32_t at = s_base[d] + s_cnt[w][d] + rank[u];
+      if (write_keys) key_out[at] = keys[u];
+      val_out[at] = vals[u];
+    }
+  }
+}
+
 struct Buf {
   void *p = nullptr;
   explicit Buf(size_t bytes) { IDX_CHECK(hipMalloc(&p, bytes < 256 ? 256 : bytes)); }
@@ -169,15 +258,13 @@ void BuildIndexDevice(const uint8_t *seq, uint32_t len, uint32_t seed, uint32_t 
     hipStream_t s;
     ~StreamGuard() { (void)hipStreamDestroy(s); }
   } sg{st};
+  const uint32_t rs_tiles = (uint32_t)(((uint64_t)len + kRsTile - 1) / kRsTile);
+  const uint32_t rs_hist_n = rs_tiles * kRsDigits;
+  const uint32_t scan_n = std::max(kcl, rs_hist_n);
   const uint32_t ntiles = (kcl + kScanTile - 1) / kScanTile;
   Buf d_seq(len), d_key(4ull * len), d_key2(4ull * len), d_val(4ull * len), d_val2(4ull * len);
-  Buf d_counts(4ull * kcl), d_tiles(4ull * ntiles);
-  size_t temp_bytes = 0;
-  const int end_bit = (int)Bits(sentinel);
-  IDX_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, d_key.as<uint32_t>(), d_key2.as<uint32_t>(),
-                                               d_val.as<uint32_t>(), d_val2.as<uint32_t>(), (int)len, 0, end_bit,
-                                               st));
-  Buf d_temp(temp_bytes);
+  Buf d_counts(4ull * kcl), d_tiles(4ull * ((scan_n + kScanTile - 1) / kScanTile)), d_hist(4ull * rs_hist_n);
+  const uint32_t end_bit = Bits(sentinel);
   hipEvent_t e0, e1;
   IDX_CHECK(hipEventCreate(&e0));
   IDX_CHECK(hipEventCreate(&e1));
@@ -200,15 +287,31 @@ void BuildIndexDevice(const uint8_t *seq, uint32_t len, uint32_t seed, uint32_t 
   hipLaunchKernelGGL(k_scan_add, dim3((kcl + kIdxBlock - 1) / kIdxBlock), dim3(kIdxBlock), 0, st,
                      d_counts.as<uint32_t>(), kcl, d_tiles.as<uint32_t>());
   IDX_CHECK(hipGetLastError());
-  IDX_CHECK(hipcub::DeviceRadixSort::SortPairs(d_temp.p, temp_bytes, d_key.as<uint32_t>(), d_key2.as<uint32_t>(),
-                                               d_val.as<uint32_t>(), d_val2.as<uint32_t>(), (int)len, 0, end_bit,
-                                               st));
+  // stable LSD radix sort of (key, j), ping-ponging between the two buffer pairs
+  uint32_t *kin = d_key.as<uint32_t>(), *vin = d_val.as<uint32_t>();
+  uint32_t *kout = d_key2.as<uint32_t>(), *vout = d_val2.as<uint32_t>();
+  const uint32_t hist_tiles = (rs_hist_n + kScanTile - 1) / kScanTile;
+  for (uint32_t shift = 0; shift < end_bit; shift += kRsBits) {
+    const bool last = shift + kRsBits >= end_bit;
+    hipLaunchKernelGGL(k_rs_hist, dim3(rs_tiles), dim3(kIdxBlock), 0, st, kin, len, shift, rs_tiles,
+                       d_hist.as<uint32_t>());
+    hipLaunchKernelGGL(k_scan_tiles, dim3(hist_tiles), dim3(kIdxBlock), 0, st, d_hist.as<uint32_t>(), rs_hist_n,
+                       d_tiles.as<uint32_t>());
+    hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(kIdxBlock), 0, st, d_tiles.as<uint32_t>(), hist_tiles);
+    hipLaunchKernelGGL(k_scan_add, dim3((rs_hist_n + kIdxBlock - 1) / kIdxBlock), dim3(kIdxBlock), 0, st,
+                       d_hist.as<uint32_t>(), rs_hist_n, d_tiles.as<uint32_t>());
+    hipLaunchKernelGGL(k_rs_scatter, dim3(rs_tiles), dim3(kIdxBlock), 0, st, kin, vin, len, shift, rs_tiles,
+                       d_hist.as<uint32_t>(), kout, vout, !last);
+    IDX_CHECK(hipGetLastError());
+    std::swap(kin, kout);
+    std::swap(vin, vout);
+  }
   IDX_CHECK(hipEventRecord(e1, st));
   IDX_CHECK(hipMemcpyAsync(keys_count, d_counts.p, 4ull * kcl, hipMemcpyDeviceToHost, st));
   IDX_CHECK(hipStreamSynchronize(st));
   const uint32_t n = keys_count[kcl - 1];
   if (n > len) throw Error("index: position count out of range");
-  if (n) IDX_CHECK(hipMemcpyAsync(positions, d_val2.p, 4ull * n, hipMemcpyDeviceToHost, st));
+  if (n) IDX_CHECK(hipMemcpyAsync(positions, vin, 4ull * n, hipMemcpyDeviceToHost, st));
   IDX_CHECK(hipStreamSynchronize(st));
   *npos = n;
   if (device_ms) IDX_CHECK(hipEventElapsedTime(device_ms, e0, e1));
