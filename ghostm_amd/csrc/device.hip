@@ -805,7 +805,8 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
     a.guard_count = reinterpret_cast<uint32_t *>(I.counters.as<unsigned long long>() + 2);
     a.guard_list = I.guard_list.as<uint32_t>();
   }
-  const size_t lds = packed ? (size_t)kern::kScoreQmax * kern::kProfRows16 * (lay.Lpad + 8) * 2
+  // packed: the profiles, then the 32 x 32 code table they are built from
+  const size_t lds = packed ? (size_t)kern::kScoreQmax * kern::kProfRows16 * (lay.Lpad + 8) * 2 + 32 * 32 * 2
                             : (size_t)kern::kScoreQmax * kern::kProfRows * (lay.Lpad + 4) * 4;
   HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
   const dim3 grid((uint32_t)ntasks), block(kern::kScoreBlock);
