@@ -1299,8 +1299,9 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
 #pragma unroll
   for (int k = 0; k < S; ++k) { H[k] = sig_prev; E[k] = sig; }
   uint32_t seen = 0;                     // halves past a true END (0xFFFF)
-  uint32_t best = 0, col = 0;
-  uint32_t jj = ((0u - i) & 0xFFFFu) * 0x10001u;
+  // col: the step of the last update per half (wave-uniform, an SGPR operand);
+  // the lane's column is step - i, taken at the end (starts at column 0)
+  uint32_t best = 0, col = (i & 0xFFFFu) * 0x10001u;
   uint32_t nend = 0;
   // what the lane below reads before this lane's first column: real 0 in its
   // frame for H (sigma(-i - 1)), and a real F below 0
@@ -1391,8 +1392,7 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
     const uint32_t cmr = W(HF(cm) - HF(sig));  // real column maximum (>= 0 off END)
     const uint32_t keep = PkSign(PkSubI16(cmr, best)) | end | fillm;
     best = BfiV(keep, best, cmr);
-    col = BfiV(keep, col, jj);
-    jj = PkAddU16(jj, 0x00010001u);
+    col = BfiV(keep, col, step * 0x10001u);
     nend = PkAddU16(nend, end | fillm);
     sig = zn;
   };
@@ -1408,8 +1408,8 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
   for (; step < steps; ++step) column(step, std::true_type{}, std::false_type{});
   const uint32_t ncolsA = steps - ((0x10000u - (nend & 0xFFFFu)) & 0xFFFFu);
   const uint32_t ncolsB = steps - ((0x10000u - (nend >> 16)) & 0xFFFFu);
-  int BA = C::Decode(best & 0xFFFFu), CA = (int)(col & 0xFFFFu);
-  int BB = C::Decode(best >> 16), CB = (int)(col >> 16);
+  int BA = C::Decode(best & 0xFFFFu), CA = (int)(((col & 0xFFFFu) - i) & 0xFFFFu);
+  int BB = C::Decode(best >> 16), CB = (int)(((col >> 16) - i) & 0xFFFFu);
   for (uint32_t k = 1; k < a.G; ++k) {
     const int src = (int)(g * a.G + k);
     const int oba = __shfl(BA, src), oca = __shfl(CA, src);
