@@ -387,6 +387,14 @@ def main() -> None:
             roof["issue_rate_ginst_s"] = rate / 1e9
             roof["measured_issue_peak_ginst_s"] = issue["packed_vop3_ginst_s"]
             roof["frac_of_measured_issue"] = rate / 1e9 / issue["packed_vop3_ginst_s"]
+            # the same in shader cycles (PMC GRBM_GUI_ACTIVE clock for both): K2's
+            # cycles per wave64 VALU instruction against the measured VOP3/VOP3P cost
+            cyc = pmc.get("k_score_valu_cycles_per_inst")
+            ref = issue.get("cycles_per_inst", {}).get("vop3_class_median")
+            if cyc and ref:
+                roof["valu_cycles_per_inst"] = cyc
+                roof["measured_vop3p_cycles_per_inst"] = ref
+                roof["effective_clock_ghz"] = pmc.get("k_score_effective_clock_ghz")
         tb_t = per["seconds_traceback"]
         tb_ach = per["traceback_cells"] * TB_OPS_PER_CELL / tb_t / 1e12 if tb_t > 0 else 0.0
         roof_k3 = {

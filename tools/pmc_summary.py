@@ -138,6 +138,11 @@ def main() -> None:
                        "VALU instructions = SQ_INSTS_VALU per dispatch",
                "k_score_hbm_bytes_per_launch": fam("k_score"),
                "k_score_valu_insts_per_launch": kernels[k2_main]["valu_insts_per_launch"] if k2_main else None,
+               # shader cycles per wave64 VALU instruction on one SIMD (GRBM_GUI_ACTIVE / 8 XCDs
+               # over the dispatch, 1024 SIMDs), the unit of profiles/r2c_valu_issue_pmc.txt
+               "k_score_valu_cycles_per_inst": (2.0 / kernels[k2_main]["valu_issue_util"])
+               if k2_main and kernels[k2_main].get("valu_issue_util") else None,
+               "k_score_effective_clock_ghz": kernels[k2_main].get("effective_clock_ghz") if k2_main else None,
                "k1_hbm_bytes_per_step": k1_step / args.trace_runs if k1 else None,
                "k1_valu_insts_per_step": k1v_step / args.trace_runs if k1v else None,
                "k1_kernels": sorted(k1)}
