@@ -75,6 +75,18 @@ def _gpu_text(q: str, db: str, aln: list) -> tuple[bytes, int]:
         return s.output(), s.stats()["query_residues"]
 
 
+def _wait(procs: list, label: str) -> list:
+    """Wait for the CPU baseline processes, logging progress every 30 s (a long
+    silent wait reads as a hung job to the GPU harness)."""
+    t0 = time.perf_counter()
+    while any(p.poll() is None for p in procs):
+        try:
+            next(p for p in procs if p.poll() is None).wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            log(f"[cpu] {label}: {time.perf_counter() - t0:.0f} s")
+    return [p.returncode for p in procs]
+
+
 def cpu_baseline(root: str, preset: str, db: str, nsample: int, aln: list) -> dict:
     """The reference's own CPU path (oracle/_ref/ghostm_ref: GHOSTM's aligner.cpp
     compiled from the reference sources, run without -D; this repo's restatement
@@ -85,7 +97,10 @@ def cpu_baseline(root: str, preset: str, db: str, nsample: int, aln: list) -> di
     q = workloads.make_queries(preset, os.path.join(root, "cpu1"), 0, nsample)
     out = os.path.join(root, "cpu1", "cpu.out")
     t0 = time.perf_counter()
-    subprocess.run([exe, "aln", "-i", q, "-d", db, "-o", out] + aln, check=True, capture_output=True)
+    p = subprocess.Popen([exe, "aln", "-i", q, "-d", db, "-o", out] + aln,
+                         stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    if _wait([p], f"1-core reference on {nsample} queries")[0] != 0:
+        raise RuntimeError("CPU baseline failed")
     dt = time.perf_counter() - t0
     gpu, residues = _gpu_text(q, db, aln)
     same = gpu == open(out, "rb").read()
@@ -114,7 +129,7 @@ def reference_split(root: str, preset: str, db: str, nsample: int, aln: list, pr
     t0 = time.perf_counter()
     running = [subprocess.Popen([exe, "aln", "-i", q, "-d", db, "-o", f"{d}/cpu.out"] + aln,
                                 stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL) for q, d in parts]
-    rcs = [p.wait() for p in running]
+    rcs = _wait(running, f"{len(running)}-process reference on {nsample} queries")
     dt = time.perf_counter() - t0
     if any(rcs):
         return None
@@ -173,8 +188,10 @@ def main() -> None:
     ap.add_argument("--preset", choices=sorted(workloads.WORKLOADS), default="cfg4",
                     help="BASELINE.json config (cfg4 = the headline workload)")
     ap.add_argument("--queries", type=int, default=None, help="queries of the whole job (default: preset)")
-    ap.add_argument("--cpu-sample", type=int, default=10000, help="queries of the 1-core CPU baseline")
-    ap.add_argument("--cpu-sample-all", type=int, default=16000, help="queries of the all-cores CPU baseline")
+    ap.add_argument("--cpu-sample", type=int, default=None,
+                    help="queries of the 1-core CPU baseline (default 10000; cfg5 4000)")
+    ap.add_argument("--cpu-sample-all", type=int, default=None,
+                    help="queries of the all-cores CPU baseline (default 16000; cfg5 8000)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--workdir", default=None)
@@ -338,8 +355,10 @@ def main() -> None:
     per = {key: v / k for key, v in st_acc.items()}
     cpu = cpu_all = None
     if rank == 0 and world == 1 and not args.no_cpu:  # the CPU baseline is an N=1 figure
-        cpu = cpu_baseline(workdir, preset, dbprefix, min(args.cpu_sample, nq), aln_args)
-        cpu_all = cpu_baseline_all_cores(workdir, preset, dbprefix, min(args.cpu_sample_all, nq), aln_args)
+        n1 = args.cpu_sample or w.get("cpu_sample", 10000)
+        nall = args.cpu_sample_all or w.get("cpu_sample_all", 16000)
+        cpu = cpu_baseline(workdir, preset, dbprefix, min(n1, nq), aln_args)
+        cpu_all = cpu_baseline_all_cores(workdir, preset, dbprefix, min(nall, nq), aln_args)
     ok = matches is not False and all(c is None or c.get("bit_identical_to_gpu_on_sample", True)
                                       for c in (cpu, cpu_all))
     if rank == 0:

@@ -36,6 +36,8 @@ WORKLOADS = {
              "workload": "cfg4: synthetic 1M queries (avg 300 aa requested, L=127) x 10M-residue DB"},
     "cfg5": {"synth": ["-s", "5", "-N", "5000000"], "queries": 100_000, "db": ("synth", 5_000_000, 5),
              "qry": ["-l", "300"], "aln": ["-r", "64", "-M", PAM250, "-y", "2"],
+             # the wide band makes the reference ~3x slower per query: smaller CPU samples
+             "cpu_sample": 4000, "cpu_sample_all": 8000,
              "workload": "cfg5: wide band -r 64, PAM250 11/1, -y 2; synthetic 100k queries x 5M-residue DB"},
 }
 
