@@ -69,8 +69,12 @@ class Session:
         native.load().GhostmSessionShardRange(self._h, ctypes.byref(b), ctypes.byref(e))
         return b.value, e.value
 
-    def run(self) -> None:
-        if native.load().GhostmSessionRun(self._h) != 0:
+    def run(self, to_file: bool = False) -> None:
+        """The search; to_file also writes the -o file while it runs
+        (GhostmSessionRunToFile), after which write() is a no-op."""
+        lib = native.load()
+        rc = lib.GhostmSessionRunToFile(self._h) if to_file else lib.GhostmSessionRun(self._h)
+        if rc != 0:
             raise GhostmError(native.last_error())
 
     def output(self) -> bytes:

@@ -235,13 +235,32 @@ void ShardCuts(uint64_t n, const uint32_t *weight, const uint8_t *group_start, u
 // Keep only this shard's queries: the chunks' queries are cut into `world`
 // contiguous ranges of about equal residues, at name-group starts (groups never
 // span chunks: the reference merges per chunk, aligner.cpp:697-700).
+// Name groups (consecutive equal names, merged into one result list:
+// aligner.cpp:697-700) and WriteOutput's query lengths of one query chunk.
+void Session::PrepareQueryChunk(QueryData *qd) {
+  QueryData &q = *qd;
+  const uint32_t n = q.chunk.nseq, L = q.chunk.L;
+  q.group_end.assign(n, 0);
+  q.group_first.clear();
+  q.group_last.clear();
+  for (uint32_t i = n; i-- > 0;) {
+    q.group_end[i] = (i + 1 < n && q.chunk.names[i + 1] == q.chunk.names[i]) ? q.group_end[i + 1] : i + 1;
+  }
+  for (uint32_t i = 0; i < n; i = q.group_end[i]) {
+    q.group_first.push_back(i);
+    q.group_last.push_back(q.group_end[i] - 1);
+  }
+  q.qlen.assign(n, 1);
+  for (uint32_t i = 0; i < n; ++i) q.qlen[i] = QueryLength(&q.chunk.seq[(size_t)i * L], L);
+}
+
 void Session::ApplyShard(uint32_t rank, uint32_t world) {
   std::vector<uint32_t> weight;
   std::vector<uint8_t> start;
   for (const QueryData &q : queries_) {
     const QueryChunk &c = q.chunk;
     for (uint32_t i = 0; i < c.nseq; ++i) {
-      weight.push_back(QueryLength(&c.seq[(size_t)i * c.L], c.L));
+      weight.push_back(q.qlen[i]);
       start.push_back(i == 0 || c.names[i] != c.names[i - 1]);
     }
   }
@@ -262,6 +281,7 @@ void Session::ApplyShard(uint32_t rank, uint32_t world) {
       c.names = std::vector<std::string>(c.names.begin() + i0, c.names.begin() + i0 + n);
       c.nseq = n;
       q.global_base += i0;
+      PrepareQueryChunk(&q);
       kept.push_back(std::move(q));
     }
     at = chunk_end;
@@ -301,11 +321,17 @@ Session::Session(const AlignerOptions &opt, uint32_t shard_rank, uint32_t shard_
   std::vector<QueryData> qread(nq_chunks);
   std::vector<DbData> dread(nd_chunks);
   std::vector<char> qok(nq_chunks, 0), dok(nd_chunks, 0);
+  // (each query chunk's name groups and WriteOutput lengths are derived on its
+  // reading thread too)
   ParallelFor(nq_chunks + nd_chunks, std::max<unsigned>(1u, std::min(threads_, 8u)),
               [&](size_t b, size_t e, unsigned) {
                 for (size_t k = b; k < e; ++k) {
-                  if (k < nq_chunks) qok[k] = qf.ReadChunk(id + (uint32_t)k, &qread[k].chunk);
-                  else dok[k - nq_chunks] = df.ReadChunk((uint32_t)(k - nq_chunks), &dread[k - nq_chunks].chunk);
+                  if (k < nq_chunks) {
+                    qok[k] = qf.ReadChunk(id + (uint32_t)k, &qread[k].chunk);
+                    if (qok[k]) PrepareQueryChunk(&qread[k]);
+                  } else {
+                    dok[k - nq_chunks] = df.ReadChunk((uint32_t)(k - nq_chunks), &dread[k - nq_chunks].chunk);
+                  }
                 }
               });
   for (uint32_t k = 0; k < nq_chunks && qok[k]; ++k) {
@@ -330,16 +356,6 @@ Session::Session(const AlignerOptions &opt, uint32_t shard_rank, uint32_t shard_
 
   for (QueryData &q : queries_) {
     const uint32_t n = q.chunk.nseq, L = q.chunk.L;
-    q.group_end.assign(n, 0);
-    for (uint32_t i = n; i-- > 0;) {
-      q.group_end[i] = (i + 1 < n && q.chunk.names[i + 1] == q.chunk.names[i]) ? q.group_end[i + 1] : i + 1;
-    }
-    for (uint32_t i = 0; i < n; i = q.group_end[i]) {
-      q.group_first.push_back(i);
-      q.group_last.push_back(q.group_end[i] - 1);
-    }
-    q.qlen.assign(n, 1);
-    for (uint32_t i = 0; i < n; ++i) q.qlen[i] = QueryLength(&q.chunk.seq[(size_t)i * L], L);
     q.dev = dev.UploadQuery(q.chunk.seq.data(), n, L);
     dev.SetQueryGroups(q.dev, q.group_first.data(), q.group_last.data(), (uint32_t)q.group_first.size());
   }
@@ -600,6 +616,7 @@ void Session::DevicePass(QueryData &q, DbData &d, const std::vector<uint32_t> &c
       FormatSelected(*qp, g0, *sel_counts, *sel_hits, cap, part);
       stats_.seconds_output += NowSeconds() - t;
       TraceMark("fmt_end", g0);
+      PartDone(part);
     });
   };
   for (size_t k = 0; k < cuts.size(); ++k) {
@@ -648,6 +665,7 @@ void Session::DevicePass(QueryData &q, DbData &d, const std::vector<uint32_t> &c
       const double t = NowSeconds();
       FormatSelected(*qp, g0, *sel_counts, *sel_hits, cap, part);
       stats_.seconds_output += NowSeconds() - t;
+      PartDone(part);
     });
   }
   finish_pending();
@@ -704,6 +722,7 @@ void Session::RunQueryChunk(QueryData &q) {
       const double t = NowSeconds();
       FormatSelected(*qp, 0, *sel_counts, *sel_hits, cap, part);
       stats_.seconds_output += NowSeconds() - t;
+      PartDone(part);
     });
   }
 }
@@ -747,7 +766,9 @@ void Session::RunQueryChunkHostMerge(QueryData &q) {
   }
   formatter_->Drain();
   const double t1 = NowSeconds();
-  FormatResults(q, results, NewPart());
+  Part *part = NewPart();
+  FormatResults(q, results, part);
+  PartDone(part);
   stats_.seconds_output += NowSeconds() - t1;
 }
 
@@ -989,9 +1010,31 @@ void Session::FormatSelected(const QueryData &q, uint32_t g0, const std::vector<
   });
 }
 
-void Session::Run() {
+void Session::Run(bool stream_to_file) {
   DeviceModule &dev = DeviceModule::Get();
   formatter_->Drain();
+  if (writer_) writer_->Drain();
+  streamed_ = false;
+  stream_failed_ = false;
+  stream_off_ = 0;
+  if (stream_to_file) {
+    if (!writer_) writer_ = std::make_unique<TaskQueue>();
+    // an unwritable path writes nothing, as the reference's unchecked ofstream
+    stream_fd_ = open(opt_.output_file.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+  }
+  struct CloseStream {  // also on an error: the writer drained, the file closed
+    Session *s;
+    ~CloseStream() {
+      if (s->stream_fd_ < 0) return;
+      try {
+        s->writer_->Drain();
+      } catch (...) {
+        s->stream_failed_ = true;
+      }
+      close(s->stream_fd_);
+      s->stream_fd_ = -1;
+    }
+  } close_stream{this};
   dev.ResetTimes();
   stats_ = GhostmStats{};
   merge_epoch_ = 0;
@@ -1012,6 +1055,12 @@ void Session::Run() {
   }
   TraceMark("drain");
   formatter_->Drain();
+  if (stream_fd_ >= 0) {
+    writer_->Drain();
+    TraceMark("streamed", stream_off_);
+    if (stream_failed_) throw Error("writing " + opt_.output_file + " failed");
+    streamed_ = true;
+  }
   stats_.seconds_total = NowSeconds() - t0;
   TraceMark("run_end");
   TraceDump();
@@ -1078,7 +1127,28 @@ size_t Session::DeviceHits(void *dst, size_t cap) {
   return n;
 }
 
+void Session::PartDone(const Part *part) {
+  if (stream_fd_ < 0) return;
+  writer_->Submit([this, part] {
+    for (const std::string &t : part->text) {
+      const char *p = t.data();
+      size_t left = t.size();
+      while (left && !stream_failed_) {
+        const ssize_t w = pwrite(stream_fd_, p, left, (off_t)stream_off_);
+        if (w <= 0) {
+          stream_failed_ = true;
+          break;
+        }
+        p += w;
+        left -= (size_t)w;
+        stream_off_ += (uint64_t)w;
+      }
+    }
+  });
+}
+
 void Session::WriteOutputFile() {
+  if (streamed_) return;  // Run(true) wrote it while searching
   TraceMark("write");
   struct Done {
     ~Done() {

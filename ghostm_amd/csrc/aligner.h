@@ -106,7 +106,10 @@ class Session {
   uint64_t ShardEnd() const { return shard_end_; }
   ~Session();
 
-  void Run();                          // whole search; replaces previous results
+  // whole search; replaces previous results. stream_to_file: also write the
+  // output file (-o) while the search runs, each segment's text as soon as it
+  // is formatted, in order (WriteOutputFile is then a no-op for this run)
+  void Run(bool stream_to_file = false);
   const std::string &Output();         // text of the last run (joined on first use)
   void WriteOutputFile();
   const std::vector<GhostmHit> &Hits();
@@ -139,6 +142,7 @@ class Session {
   };
   using Results = std::vector<std::vector<HitRecord>>;
 
+  static void PrepareQueryChunk(QueryData *q);
   void ApplyShard(uint32_t rank, uint32_t world);
   void RunQueryChunk(QueryData &q);
   void RunQueryChunkHostMerge(QueryData &q);
@@ -152,6 +156,8 @@ class Session {
   void FormatSelected(const QueryData &q, uint32_t g0, const std::vector<uint32_t> &counts,
                       const HostHits &hits, uint32_t cap, Part *out);
   Part *NewPart();
+  // a part's text is complete: hands it to the output writer when streaming
+  void PartDone(const Part *part);
   const LineFormat &Format();
 
   AlignerOptions opt_;
@@ -170,6 +176,10 @@ class Session {
   GhostmStats stats_{};
   unsigned threads_ = 1;
   std::unique_ptr<TaskQueue> formatter_;
+  std::unique_ptr<TaskQueue> writer_;  // streamed output (Run(true)), in part order
+  int stream_fd_ = -1;
+  uint64_t stream_off_ = 0;
+  bool stream_failed_ = false, streamed_ = false;
   std::unique_ptr<LineFormat> format_;
 };
 

@@ -68,6 +68,17 @@ int GhostmSessionRun(void *s) {
   }
 }
 
+int GhostmSessionRunToFile(void *s) {
+  try {
+    if (!s) throw Error("null session");
+    static_cast<Session *>(s)->Run(true);
+    return 0;
+  } catch (std::exception &e) {
+    SetLastErrorMessage(e.what());
+    return 1;
+  }
+}
+
 size_t GhostmSessionOutput(void *s, char *buf, size_t cap) {
   if (!s) return 0;
   const std::string &o = static_cast<Session *>(s)->Output();
@@ -122,8 +133,8 @@ int GhostmAlignMain(int argc, char **argv) {
     AlignerOptions opt = ParseAlignerOptions(argc, argv);
     { std::ofstream touch(opt.output_file.c_str()); }
     Session session(opt);
-    session.Run();
-    session.WriteOutputFile();
+    session.Run(true);       // the output file is written while the search runs
+    session.WriteOutputFile();  // no-op after a streamed run
     if (opt.verbose) {
       const GhostmStats &st = session.Stats();
       std::cout << "# queries " << st.queries << " candidates " << st.candidates << " hits "

@@ -112,6 +112,7 @@ SIGNATURES = {
     "GhostmSessionShardRange": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
     "GhostmShardCuts": (c_int, [c_uint64, u32p, POINTER(ctypes.c_uint8), c_int, POINTER(c_uint64)]),
     "GhostmSessionRun": (c_int, [c_void_p]),
+    "GhostmSessionRunToFile": (c_int, [c_void_p]),
     "GhostmSessionOutput": (c_size_t, [c_void_p, c_char_p, c_size_t]),
     "GhostmSessionWrite": (c_int, [c_void_p]),
     "GhostmSessionHits": (c_size_t, [c_void_p, POINTER(GhostmHit), c_size_t]),

@@ -233,6 +233,12 @@ int GhostmShardCuts(uint64_t n, const uint32_t weights[], const uint8_t group_st
  * tie rules) on the device. Results replace those of any previous run. */
 int GhostmSessionRun(void *session);
 
+/* GhostmSessionRun that also writes the -o file while the search runs: each
+ * segment's text is written, in output order, as soon as it is formatted (the
+ * reference writes after each query chunk, aligner.cpp:211). The file equals
+ * what GhostmSessionWrite writes; GhostmSessionWrite is then a no-op. */
+int GhostmSessionRunToFile(void *session);
+
 /* Formatted output of the last run (reference WriteOutput/V1/V2 text). With
  * buf == NULL returns the byte count; otherwise copies min(cap, size) bytes. */
 size_t GhostmSessionOutput(void *session, char *buf, size_t cap);

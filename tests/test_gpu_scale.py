@@ -120,6 +120,54 @@ def test_many_segment_device_pipeline(ds, var, opts, seg, tail, dataset, golden)
     assert dev.tobytes() == hits.tobytes()
 
 
+@pytest.mark.parametrize("merge", ["device", "host"])
+@pytest.mark.parametrize("ds,var,opts", [("syn_small", "default", []), ("syn_dna", "default", []),
+                                         ("syn_chunks", "default", [])])
+def test_streamed_output_file(merge, ds, var, opts, dataset, golden, tmp_path):
+    """GhostmSessionRunToFile writes the -o file while the search runs (each
+    segment's text as soon as it is formatted, in order): the file is the
+    reference output over many segments, on the device-merge and host-merge
+    paths, and a later write() leaves it as it is."""
+    d = dataset(ds)
+    env = {"GHOSTM_SEGMENT_CANDS": "300", "GHOSTM_TAIL_CANDS": "40"}
+    if merge == "host":
+        env["GHOSTM_MERGE"] = "host"
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    out = tmp_path / "streamed.out"
+    out.write_bytes(b"stale bytes that must be truncated " * 1000)
+    try:
+        with Session(["-i", os.path.join(d, "q"), "-d", os.path.join(d, "db"), "-o", str(out), "-D", "0"]
+                     + list(opts)) as s:
+            s.run(to_file=True)
+            text = s.output()
+            assert out.read_bytes() == text
+            s.write()
+            assert out.read_bytes() == text
+            s.run()  # a plain run after a streamed one: write() writes again
+            out.unlink()
+            s.write()
+            assert out.read_bytes() == text
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    assert _sha(text) == golden["aln"][f"{ds}/{var}"]["sha256"]
+
+
+def test_streamed_output_unwritable_path(dataset, tmp_path):
+    """As the reference's unchecked ofstream: an -o path that cannot be opened
+    writes nothing and the run still succeeds."""
+    d = dataset("syn_small")
+    bad = str(tmp_path / "no_such_dir" / "x.out")
+    with Session(["-i", os.path.join(d, "q"), "-d", os.path.join(d, "db"), "-o", bad, "-D", "0"]) as s:
+        s.run(to_file=True)
+        assert len(s.output()) > 0
+    assert not os.path.exists(bad)
+
+
 # ----------------------------------------------------------- full workloads
 FULL = os.path.join(cases.GOLDEN, "full_golden.json")
 
