@@ -1171,9 +1171,12 @@ void DeviceModule::MergeLaunch(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, 
   m.wave_cap = kern::kMergeCap;
   if (const char *c = getenv("GHOSTM_K4_CAP"))  // tests: send smaller groups to the one-lane fallback
     m.wave_cap = std::min<uint32_t>((uint32_t)strtoul(c, nullptr, 10), kern::kMergeCap);
-  if (wave)
-    hipLaunchKernelGGL(kern::k_merge_wave, dim3((ng + kern::kMergeWaves - 1) / kern::kMergeWaves),
-                       dim3(64 * kern::kMergeWaves), 0, S(stream_), m);
+  if (wave) {
+    // persistent: three workgroups per CU fit the LDS (53 KB each)
+    const uint32_t blocks = std::max<uint32_t>(
+        1, std::min<uint32_t>((ng + kern::kMergeWaves - 1) / kern::kMergeWaves, (uint32_t)I.cus * 3));
+    hipLaunchKernelGGL(kern::k_merge_wave, dim3(blocks), dim3(64 * kern::kMergeWaves), 0, S(stream_), m);
+  }
   else
     hipLaunchKernelGGL(kern::k_merge, dim3((ng + 255) / 256), dim3(256), 0, S(stream_), m);
   times_.merge_launches += 1;

@@ -1977,15 +1977,10 @@ __device__ void WaveStableSort(unsigned long long *K, uint32_t first, uint32_t l
   WaveSync();
 }
 
-__global__ __launch_bounds__(64 * kMergeWaves) void k_merge_wave(MergeArgs a) {
-  __shared__ unsigned long long s_key[kMergeWaves][kMergeCap];
-  __shared__ uint16_t s_ls[kMergeWaves][kMergeCap + 2];
-  __shared__ uint16_t s_rs[kMergeWaves][kMergeCap + 2];
-  __shared__ MergeFrame s_stack[kMergeWaves][64];
-  __shared__ uint32_t s_taken[kMergeWaves][kMergeBest];
-  const uint32_t lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t g = blockIdx.x * kMergeWaves + w;
-  if (g >= a.ng) return;
+// One name group on one wave (K, stop lists, stack and taken list: the wave's
+// LDS rows).
+__device__ inline void MergeWaveGroup(const MergeArgs &a, uint32_t g, uint32_t lane, unsigned long long *K,
+                                      uint16_t *ls, uint16_t *rs, MergeFrame *stk, uint32_t *taken) {
   unsigned long long b, n64;
   GroupRange(a, g, &b, &n64);
   const size_t so = (size_t)g * a.cap;
@@ -1995,12 +1990,9 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_merge_wave(MergeArgs a) {
     return;
   }
   const uint32_t nnew = (uint32_t)n64, n = nnew + nc;
-  unsigned long long *K = s_key[w];
   for (uint32_t i = lane; i < nnew; i += 64) K[i] = ((unsigned long long)a.score[b + i] << 32) | i;
   for (uint32_t k = lane; k < nc; k += 64)
     K[nnew + k] = ((unsigned long long)a.carry[so + k].score << 32) | (nnew + k);
-  MergeFrame *stk = s_stack[w];
-  uint32_t *taken = s_taken[w];
   if (lane == 0 && n) stk[0] = MergeFrame{0u, n, 2 * stdsort::Lg((long)n)};
   int sp = n ? 1 : 0;
   WaveSync();
@@ -2023,7 +2015,7 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_merge_wave(MergeArgs a) {
         const uint32_t mid = f.first + (f.last - f.first) / 2;
         if (lane == 0) stdsort::MoveMedianToFirst(K + f.first, K + f.first + 1, K + mid, K + f.last - 1, less);
         WaveSync();
-        const uint32_t cut = WavePartition(K, f.first, f.last, s_ls[w], s_rs[w], lane);
+        const uint32_t cut = WavePartition(K, f.first, f.last, ls, rs, lane);
         if (lane == 0) stk[sp] = MergeFrame{cut, f.last, f.depth};
         ++sp;
         f.last = cut;
@@ -2075,6 +2067,23 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_merge_wave(MergeArgs a) {
   }
   if (lane == 0) a.sel_count[g] = count;
   for (uint32_t k = count + lane; k < a.cap; k += 64) a.tb_qid[so + k] = 0xFFFFFFFFu;
+}
+
+// Persistent: a grid of a few workgroups per CU (as many as the LDS rows allow
+// at once), each wave taking every (grid waves)-th group; one launch per group
+// kept only ~2 waves per CU resident (the dispatch rate, not the LDS, bound it).
+__global__ __launch_bounds__(64 * kMergeWaves) void k_merge_wave(MergeArgs a) {
+  __shared__ unsigned long long s_key[kMergeWaves][kMergeCap];
+  __shared__ uint16_t s_ls[kMergeWaves][kMergeCap + 2];
+  __shared__ uint16_t s_rs[kMergeWaves][kMergeCap + 2];
+  __shared__ MergeFrame s_stack[kMergeWaves][64];
+  __shared__ uint32_t s_taken[kMergeWaves][kMergeBest];
+  const uint32_t lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t stride = gridDim.x * kMergeWaves;
+  for (uint32_t g = blockIdx.x * kMergeWaves + w; g < a.ng; g += stride) {
+    MergeWaveGroup(a, g, lane, s_key[w], s_ls[w], s_rs[w], s_stack[w], s_taken[w]);
+    WaveSync();
+  }
 }
 
 // Selected slots -> records: a new hit rebased to its subject after K3, a
