@@ -28,6 +28,21 @@ namespace ghostm {
 
 namespace {
 
+// Page-locked host staging (hipHostMalloc), grown on demand, never shrunk.
+struct PinnedBuf {
+  void *p = nullptr;
+  size_t bytes = 0;
+  void Reserve(size_t b) {
+    if (b <= bytes) return;
+    if (p) HIP_CHECK(hipHostFree(p));
+    p = nullptr;
+    bytes = 0;
+    HIP_CHECK(hipHostMalloc(&p, std::max<size_t>(b, 256), hipHostMallocDefault));
+    bytes = std::max<size_t>(b, 256);
+  }
+  template <class T> T *as() const { return static_cast<T *>(p); }
+};
+
 struct DevBuf {
   void *p = nullptr;
   size_t bytes = 0;
@@ -143,6 +158,9 @@ struct DeviceModule::Impl {
   hipEvent_t ev_m0 = nullptr, ev_m1 = nullptr;      // K4
   hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;      // K3
   hipEvent_t ev_done = nullptr, ev_tasks = nullptr; // end of a segment's selection; next tasks uploaded
+  // K1 read-backs (per-query bin and candidate counts) land in page-locked
+  // staging: GHOSTM_K1_PINNED=0 keeps the pageable copies (A/B)
+  PinnedBuf h_nbins, h_counts, h_qlist;
   DevBuf counters;     // K2: u64 [0] score cells, u32 at [2] guard count
   DevBuf tb_counters;  // K3: u64 [0] traceback cells, [1] K3a scan cells
   bool matrix_set = false;
@@ -502,38 +520,64 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
   hipLaunchKernelGGL(kern::k_seed_lists, dim3((nq + 3) / 4), dim3(256), 0, S(stream_), la);
   HIP_CHECK(hipGetLastError());
   TraceMark("k1a_launch");
-  std::vector<uint32_t> nbins(nq);
-  HIP_CHECK(hipMemcpyAsync(nbins.data(), I.nelem.p, (size_t)nq * 4, hipMemcpyDeviceToHost, S(stream_)));
+  const char *pin_env = getenv("GHOSTM_K1_PINNED");
+  const bool pinned = !(pin_env && strcmp(pin_env, "0") == 0);
+  std::vector<uint32_t> nbins_v;
+  const uint32_t *nbins = nullptr;
+  if (pinned) {
+    I.h_nbins.Reserve((size_t)nq * 4);
+    HIP_CHECK(hipMemcpyAsync(I.h_nbins.p, I.nelem.p, (size_t)nq * 4, hipMemcpyDeviceToHost, S(stream_)));
+    nbins = I.h_nbins.as<uint32_t>();
+  } else {
+    nbins_v.resize(nq);
+    HIP_CHECK(hipMemcpyAsync(nbins_v.data(), I.nelem.p, (size_t)nq * 4, hipMemcpyDeviceToHost, S(stream_)));
+    nbins = nbins_v.data();
+  }
   TraceMark("k1a_enq");
   HIP_CHECK(hipStreamSynchronize(S(stream_)));
   TraceMark("k1a_done");
 
-  // size classes (queries without any position keep count 0)
-  std::vector<uint32_t> cls[4];
-  std::vector<unsigned long long> goff;
-  unsigned long long gtotal = 0;
+  // size classes (queries without any position keep count 0): one counting
+  // pass, then the lists written by class straight into page-locked staging
+  // (cls[c] views it) and uploaded asynchronously
+  uint32_t ncls[4] = {0, 0, 0, 0};
   uint64_t bins_total = 0;
+  auto class_of = [&](uint32_t n) { return n <= caps[0] ? 0 : n <= caps[1] ? 1 : n <= caps[2] ? 2 : 3; };
   for (uint32_t i = 0; i < nq; ++i) {
     const uint32_t n = nbins[i];
     bins_total += n;
-    if (n == 0) continue;
-    int c = 3;
-    for (int k = 0; k < 3; ++k)
-      if (n <= caps[k]) { c = k; break; }
-    cls[c].push_back(i);
-    if (c == 3) {
-      goff.push_back(gtotal);
-      gtotal += 2ull * n;
-    }
+    if (n) ++ncls[class_of(n)];
   }
-  size_t list_total = 0;
-  for (auto &v : cls) list_total += v.size();
+  const size_t list_total = (size_t)ncls[0] + ncls[1] + ncls[2] + ncls[3];
+  I.h_qlist.Reserve(list_total * 4 + 4);
+  uint32_t *hl = I.h_qlist.as<uint32_t>();
+  struct Span {
+    const uint32_t *p;
+    size_t n;
+    const uint32_t *begin() const { return p; }
+    const uint32_t *end() const { return p + n; }
+    size_t size() const { return n; }
+  } cls[4];
+  {
+    uint32_t at[4];
+    size_t o = 0;
+    for (int c = 0; c < 4; ++c) {
+      cls[c] = Span{hl + o, ncls[c]};
+      at[c] = (uint32_t)o;
+      o += ncls[c];
+    }
+    for (uint32_t i = 0; i < nq; ++i)
+      if (nbins[i]) hl[at[class_of(nbins[i])]++] = i;
+  }
+  std::vector<unsigned long long> goff;  // class 3: global merge buffer offsets
+  unsigned long long gtotal = 0;
+  for (uint32_t qi : cls[3]) {
+    goff.push_back(gtotal);
+    gtotal += 2ull * nbins[qi];
+  }
   I.qlist.Reserve(list_total * 4 + 4);
-  std::vector<uint32_t> pass1;  // outlives the async copy (synchronised below)
-  pass1.reserve(list_total);
-  for (auto &v : cls) pass1.insert(pass1.end(), v.begin(), v.end());
-  if (!pass1.empty())
-    HIP_CHECK(hipMemcpyAsync(I.qlist.p, pass1.data(), pass1.size() * 4, hipMemcpyHostToDevice, S(stream_)));
+  if (list_total)
+    HIP_CHECK(hipMemcpyAsync(I.qlist.p, hl, list_total * 4, hipMemcpyHostToDevice, S(stream_)));
   if (gtotal) {
     I.gbuf.Reserve(gtotal * 4);
     I.gbuf_off.Reserve(goff.size() * 8);
@@ -574,9 +618,15 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
   }
   times_.seed_launches_hash += hash ? 1 : 0;
   times_.seed_launches_filter += filter ? 1 : 0;
-  HIP_CHECK(hipMemcpyAsync(counts->data(), I.counts.p, (size_t)nq * 4, hipMemcpyDeviceToHost, S(stream_)));
+  if (pinned) {
+    I.h_counts.Reserve((size_t)nq * 4);
+    HIP_CHECK(hipMemcpyAsync(I.h_counts.p, I.counts.p, (size_t)nq * 4, hipMemcpyDeviceToHost, S(stream_)));
+  } else {
+    HIP_CHECK(hipMemcpyAsync(counts->data(), I.counts.p, (size_t)nq * 4, hipMemcpyDeviceToHost, S(stream_)));
+  }
   TraceMark("k1b_enq");
   HIP_CHECK(hipStreamSynchronize(S(stream_)));
+  if (pinned) std::memcpy(counts->data(), I.h_counts.p, (size_t)nq * 4);
   TraceMark("k1b_done");
   if (filter) {
     // queries whose filtered queue overflowed: the unfiltered table redoes them
