@@ -144,3 +144,54 @@ def test_index_abi_errors():
     assert "keys_count" in last_error()
     assert lib.GhostmBuildIndexGpu(p8, 6, 15, 32 ** 4 + 1, u32(kc), u32(pos), ctypes.byref(npos), 0, None) == 0
     assert npos.value == 2 and kc[-1] == 2
+
+
+def _restated_index_solid(seq: np.ndarray, span: int = 4):
+    """Vectorised ConstructIndex for a solid seed of `span` ones (the rule of
+    _restated_index, db_creator.cpp:183-233), for sizes the loop is too slow for."""
+    n = len(seq)
+    kcl = 32 ** span + 1
+    m = n - span  # windows with j + span < n (the chunk ends with an END)
+    if m <= 0:
+        return np.zeros(kcl, dtype=np.uint32), np.zeros(0, dtype=np.uint32)
+    bad = ((seq == 25) | (seq == 23)).astype(np.int32)
+    cb = np.concatenate([[0], np.cumsum(bad)])
+    j = np.arange(m)
+    ok = (cb[j + span] - cb[j]) == 0
+    starts_subject = (j == 0) | (seq[np.maximum(j - 1, 0)] == 25)
+    ok &= ~(starts_subject & (seq[j + span] == 25))
+    keys = np.zeros(m, dtype=np.int64)
+    for t in range(span):
+        keys = (keys << 5) | seq[j + t].astype(np.int64)
+    keys, pos = keys[ok], j[ok].astype(np.uint32)
+    order = np.argsort(keys, kind="stable")
+    kc = np.zeros(kcl, dtype=np.uint32)
+    np.add.at(kc, keys + 1, 1)
+    return np.cumsum(kc, dtype=np.uint32), pos[order]
+
+
+@pytest.mark.parametrize("n", [2, 65, 4095, 4096, 4097, 8193, 250001])
+def test_index_radix_sort_tile_edges(n):
+    """The hand-written radix sort (index.hip k_rs_*) at lengths around its
+    4096-element tiles and 64-element batches: CSR and positions equal a numpy
+    stable sort of the same windows."""
+    from ghostm_amd.native import load, last_error
+
+    rng = np.random.default_rng(n)
+    seq = rng.integers(0, 23, size=n).astype(np.uint8)
+    seq[rng.random(n) < 0.004] = 23  # X
+    seq[rng.random(n) < 0.01] = 25   # subject ends
+    seq[-1] = 25
+    want_kc, want_pos = _restated_index_solid(seq)
+    lib = load()
+    kcl = 32 ** 4 + 1
+    kc = np.zeros(kcl, dtype=np.uint32)
+    pos = np.zeros(n, dtype=np.uint32)
+    npos = ctypes.c_uint32(0)
+    u32 = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))  # noqa: E731
+    rc = lib.GhostmBuildIndexGpu(seq.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), n, 0b1111, kcl,
+                                 u32(kc), u32(pos), ctypes.byref(npos), 0, None)
+    assert rc == 0, last_error()
+    assert np.array_equal(kc, want_kc)
+    assert npos.value == len(want_pos)
+    assert np.array_equal(pos[:npos.value], want_pos)
