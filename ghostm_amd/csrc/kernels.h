@@ -2464,38 +2464,60 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
       const char *tp = reinterpret_cast<const char *>(s_pair) + cbase;
       auto T = [&](int u) { return *reinterpret_cast<const uint32_t *>(tp + ((qoff[u >> 2] >> (8 * (u & 3))) & 0xFFu)); };
       uint32_t diag = diag0, F = fin, cm = sig;
+      if constexpr (FRAMED) {
+        // software-pipelined by chunks of four rows: the next chunk's four table
+        // reads are issued before this chunk's rows, and each row's diagonal
+        // sum is formed one row ahead, from the old H just before the row above
+        // overwrites it (t + tn + two sums: fewer live registers than eight
+        // reads and eight sums)
+        constexpr int CH = 4;
+        uint32_t t[CH], tn[CH];
+#pragma unroll
+        for (int u = 0; u < CH; ++u) t[u] = T(u);
+        uint32_t sc = W(HF(diag) + HF(t[0]));
+#pragma unroll
+        for (int k = 0; k < S; k += CH) {
+          if (k + CH < S) {
+#pragma unroll
+            for (int u = 0; u < CH; ++u) tn[u] = T(k + CH + u);
+          }
+#pragma unroll
+          for (int u = 0; u < CH; ++u) {
+            uint32_t sn = 0;
+            if (u < CH - 1) sn = W(HF(H[k + u]) + HF(t[u + 1]));
+            else if (k + CH < S) sn = W(HF(H[k + u]) + HF(tn[0]));
+            const hf2 h = __builtin_elementwise_maximum(__builtin_elementwise_maximum(HF(sc), HF(E[k + u])), HF(F));
+            H[k + u] = W(h);
+            const hf2 oE = h + KOE;
+            const hf2 G = __builtin_elementwise_maximum(HF(F), oE);
+            E[k + u] = W(__builtin_elementwise_maximum(__builtin_elementwise_maximum(HF(E[k + u]), oE), Z1));
+            F = W(G + NEXT);
+            sc = sn;
+          }
+          cm = C::Max3(C::Max3(H[k], H[k + 1], H[k + 2]), H[k + 3], cm);
+          if (k + CH < S) {
+#pragma unroll
+            for (int u = 0; u < CH; ++u) t[u] = tn[u];
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
 #pragma unroll
       for (int k = 0; k < S; k += 8) {
         // the chunk's eight table reads issued together, then their sums
         uint32_t t[8], s[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) t[u] = T(k + u);
-        if constexpr (FRAMED) {
 #pragma unroll
-          for (int u = 0; u < 8; ++u) s[u] = W(HF(u == 0 ? diag : H[k + u - 1]) + HF(t[u]));
-        } else {
-#pragma unroll
-          for (int u = 0; u < 8; ++u) s[u] = C::Diag(u == 0 ? diag : H[k + u - 1], st.m, t[u]);
-        }
+        for (int u = 0; u < 8; ++u) s[u] = C::Diag(u == 0 ? diag : H[k + u - 1], st.m, t[u]);
         diag = H[k + 7];
-        if constexpr (FRAMED) {
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            const hf2 h = __builtin_elementwise_maximum(__builtin_elementwise_maximum(HF(s[u]), HF(E[k + u])), HF(F));
-            H[k + u] = W(h);
-            const hf2 oE = h + KOE;
-            const hf2 G = __builtin_elementwise_maximum(HF(F), oE);
-            E[k + u] = W(__builtin_elementwise_maximum(__builtin_elementwise_maximum(HF(E[k + u]), oE), Z1));
-            F = W(G + NEXT);
-          }
-        } else {
-#pragma unroll
-          for (int u = 0; u < 8; ++u) C::Row(st, s[u], H[k + u], E[k + u], F);
-        }
+        for (int u = 0; u < 8; ++u) C::Row(st, s[u], H[k + u], E[k + u], F);
         cm = C::Max3(C::Max3(H[k], H[k + 1], H[k + 2]), C::Max3(H[k + 3], H[k + 4], H[k + 5]),
                      C::Max3(H[k + 6], H[k + 7], cm));
         // the next chunk's table reads stay behind this one (register budget)
         __builtin_amdgcn_sched_barrier(0);
+      }
       }
       hout = H[S - 1];
       fout = F;
