@@ -1100,6 +1100,7 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
     a.order = I.tb_order2.as<uint32_t>();
     a.ncols = I.tb_ncols.as<uint32_t>();
     a.best_h = I.tb_best.as<uint32_t>();
+    a.rcodes = q->rcodes.as<uint32_t>();  // built for this Lpad just above
     times_.traceback_launches_scan += 1;
   }
   const uint32_t per_block = (kern::kTbBlock / 64) * lay.gpw;

@@ -1467,6 +1467,9 @@ struct TbArgs {
   // with ncols: each hit's maximum from the scan; the key kernel then keeps no
   // running maximum and reads the first maximal cell off column j* at the end
   const uint32_t *best_h;
+  // k_rev_codes' packed row offsets of every query (per query Lpad / 4 words),
+  // when the scan made them; null = built from qseq bytes
+  const uint32_t *rcodes;
 };
 
 // the wave's largest value (loop bound of a lane-group loop)
@@ -1640,12 +1643,24 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
     p0 = a.end[hit];
     width = p0 < a.base ? p0 + 1 : a.base;
     if (a.ncols) width = min(width, a.ncols[hit]);
-    const uint8_t *qs = a.qseq + (size_t)a.qid[hit] * a.L;
+    if (S >= 16 && a.rcodes) {  // the same bytes, four rows per word, from k_rev_codes
+      const uint4 *rw = reinterpret_cast<const uint4 *>(a.rcodes + (size_t)a.qid[hit] * (a.Lpad / 4) + i * (S / 4));
 #pragma unroll
-    for (int u = 0; u < S; ++u) {
-      const int k = (int)a.Lpad - 1 - (int)(i * S + u);
-      const uint32_t off = (k >= 0 && k < (int)a.L) ? (uint32_t)qs[k] * 4 : kPadCode * 4;
-      qoff[u >> 2] = (qoff[u >> 2] & ~(0xFFu << (8 * (u & 3)))) | (off << (8 * (u & 3)));
+      for (int w = 0; w < S / 16; ++w) {
+        const uint4 v = rw[w];
+        qoff[4 * w] = v.x;
+        qoff[4 * w + 1] = v.y;
+        qoff[4 * w + 2] = v.z;
+        qoff[4 * w + 3] = v.w;
+      }
+    } else {
+      const uint8_t *qs = a.qseq + (size_t)a.qid[hit] * a.L;
+#pragma unroll
+      for (int u = 0; u < S; ++u) {
+        const int k = (int)a.Lpad - 1 - (int)(i * S + u);
+        const uint32_t off = (k >= 0 && k < (int)a.L) ? (uint32_t)qs[k] * 4 : kPadCode * 4;
+        qoff[u >> 2] = (qoff[u >> 2] & ~(0xFFu << (8 * (u & 3)))) | (off << (8 * (u & 3)));
+      }
     }
   }
   int K[S], KE[S];
