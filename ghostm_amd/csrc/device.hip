@@ -1223,10 +1223,16 @@ void DeviceModule::MergeLaunch(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, 
   if (const char *c = getenv("GHOSTM_K4_CAP"))  // tests: send smaller groups to the one-lane fallback
     m.wave_cap = std::min<uint32_t>((uint32_t)strtoul(c, nullptr, 10), kern::kMergeCap);
   if (wave) {
-    // persistent: three workgroups per CU fit the LDS (53 KB each)
-    const uint32_t blocks = std::max<uint32_t>(
-        1, std::min<uint32_t>((ng + kern::kMergeWaves - 1) / kern::kMergeWaves, (uint32_t)I.cus * 3));
-    hipLaunchKernelGGL(kern::k_merge_wave, dim3(blocks), dim3(64 * kern::kMergeWaves), 0, S(stream_), m);
+    // persistent: groups of up to 512 keys in 29 KB workgroups (five per CU),
+    // then the larger ones in 53 KB workgroups (three per CU)
+    m.wave_small = std::min<uint32_t>(kern::kMergeSmall, m.wave_cap);
+    const uint32_t want = (ng + kern::kMergeWaves - 1) / kern::kMergeWaves;
+    const uint32_t small = std::max<uint32_t>(1, std::min<uint32_t>(want, (uint32_t)I.cus * 5));
+    const uint32_t large = std::max<uint32_t>(1, std::min<uint32_t>(want, (uint32_t)I.cus * 3));
+    hipLaunchKernelGGL((kern::k_merge_wave<kern::kMergeSmall, true>), dim3(small), dim3(64 * kern::kMergeWaves), 0,
+                       S(stream_), m);
+    hipLaunchKernelGGL((kern::k_merge_wave<kern::kMergeCap, false>), dim3(large), dim3(64 * kern::kMergeWaves), 0,
+                       S(stream_), m);
   }
   else
     hipLaunchKernelGGL(kern::k_merge, dim3((ng + 255) / 256), dim3(256), 0, S(stream_), m);

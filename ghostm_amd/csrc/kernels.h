@@ -1806,6 +1806,7 @@ struct MergeArgs {
   uint32_t *tb_qid;                    // [ng*cap] K3 request (0xFFFFFFFF = empty)
   uint32_t *tb_end;                    // [ng*cap]
   uint32_t wave_cap;                   // k_merge_wave: largest group kept in LDS (<= kMergeCap)
+  uint32_t wave_small;                 // k_merge_wave: the small launch's largest group
   // the batch's candidate range (absolute): a group's candidates are its
   // queries' candidates clipped to it (a batch may cut a name group)
   unsigned long long cand_lo, cand_hi;
@@ -1918,6 +1919,7 @@ __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
 // k_merge. The walk then takes up to 64 finalized keys at a time: subjects by
 // binary search in parallel, first occurrences by lane order.
 constexpr uint32_t kMergeCap = 1024;   // keys per wave in LDS
+constexpr uint32_t kMergeSmall = 512;  // the small-group launch's keys per wave (more waves per CU)
 constexpr uint32_t kMergeWaves = 4;    // groups per workgroup
 constexpr uint32_t kMergeBest = 64;    // largest -b k_merge_wave takes
 
@@ -1994,15 +1996,23 @@ __device__ void WaveStableSort(unsigned long long *K, uint32_t first, uint32_t l
 
 // One name group on one wave (K, stop lists, stack and taken list: the wave's
 // LDS rows).
+// SMALL: only groups of at most a.wave_small keys; otherwise only the larger
+// ones (in LDS up to a.wave_cap, beyond on one lane as k_merge).
+template <bool SMALL>
 __device__ inline void MergeWaveGroup(const MergeArgs &a, uint32_t g, uint32_t lane, unsigned long long *K,
                                       uint16_t *ls, uint16_t *rs, MergeFrame *stk, uint32_t *taken) {
   unsigned long long b, n64;
   GroupRange(a, g, &b, &n64);
   const size_t so = (size_t)g * a.cap;
   const uint32_t nc = a.carry_count ? a.carry_count[g] : 0u;
-  if (n64 + nc > a.wave_cap) {
-    if (lane == 0) MergeGroup(a, g);
-    return;
+  if (SMALL) {
+    if (n64 + nc > a.wave_small) return;
+  } else {
+    if (n64 + nc <= a.wave_small) return;
+    if (n64 + nc > a.wave_cap) {
+      if (lane == 0) MergeGroup(a, g);
+      return;
+    }
   }
   const uint32_t nnew = (uint32_t)n64, n = nnew + nc;
   for (uint32_t i = lane; i < nnew; i += 64) K[i] = ((unsigned long long)a.score[b + i] << 32) | i;
@@ -2085,18 +2095,20 @@ __device__ inline void MergeWaveGroup(const MergeArgs &a, uint32_t g, uint32_t l
 }
 
 // Persistent: a grid of a few workgroups per CU (as many as the LDS rows allow
-// at once), each wave taking every (grid waves)-th group; one launch per group
-// kept only ~2 waves per CU resident (the dispatch rate, not the LDS, bound it).
+// at once), each wave taking every (grid waves)-th group. Two launches: CAP =
+// kMergeSmall for the groups of at most a.wave_small keys (about twice the
+// waves per CU of the 1024-key rows), then CAP = kMergeCap for the rest.
+template <uint32_t CAP, bool SMALL>
 __global__ __launch_bounds__(64 * kMergeWaves) void k_merge_wave(MergeArgs a) {
-  __shared__ unsigned long long s_key[kMergeWaves][kMergeCap];
-  __shared__ uint16_t s_ls[kMergeWaves][kMergeCap + 2];
-  __shared__ uint16_t s_rs[kMergeWaves][kMergeCap + 2];
+  __shared__ unsigned long long s_key[kMergeWaves][CAP];
+  __shared__ uint16_t s_ls[kMergeWaves][CAP + 2];
+  __shared__ uint16_t s_rs[kMergeWaves][CAP + 2];
   __shared__ MergeFrame s_stack[kMergeWaves][64];
   __shared__ uint32_t s_taken[kMergeWaves][kMergeBest];
   const uint32_t lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t stride = gridDim.x * kMergeWaves;
   for (uint32_t g = blockIdx.x * kMergeWaves + w; g < a.ng; g += stride) {
-    MergeWaveGroup(a, g, lane, s_key[w], s_ls[w], s_rs[w], s_stack[w], s_taken[w]);
+    MergeWaveGroup<SMALL>(a, g, lane, s_key[w], s_ls[w], s_rs[w], s_stack[w], s_taken[w]);
     WaveSync();
   }
 }
