@@ -1036,7 +1036,8 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
     hipLaunchKernelGGL(kern::k_tb_pairs, dim3((uint32_t)((runs + 255) / 256)), b256, 0, S(stream_), a.qid,
                        I.tb_width.as<uint32_t>(), n, ps, I.tb_pair_a.as<uint32_t>(), I.tb_pair_b.as<uint32_t>(),
                        I.tb_key.as<uint32_t>(), hist1);
-    hipLaunchKernelGGL(kern::k_csort_scatter, g256, b256, 0, S(stream_), I.tb_key.as<uint32_t>(), n, true,
+    const dim3 gsort((n + kern::kCsortTile - 1) / kern::kCsortTile);
+    hipLaunchKernelGGL(kern::k_csort_scatter, gsort, b256, 0, S(stream_), I.tb_key.as<uint32_t>(), n, true,
                        hist1, cur1, I.tb_order1.as<uint32_t>());
     kern::TbScanArgs sa{};
     sa.qseq = a.qseq;
@@ -1094,7 +1095,7 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
     }
 #undef GHOSTM_SCAN
 #undef GHOSTM_SCAN1
-    hipLaunchKernelGGL(kern::k_csort_scatter, g256, b256, 0, S(stream_), I.tb_ncols.as<uint32_t>(), n, false,
+    hipLaunchKernelGGL(kern::k_csort_scatter, gsort, b256, 0, S(stream_), I.tb_ncols.as<uint32_t>(), n, false,
                        hist2, cur2, I.tb_order2.as<uint32_t>());
     HIP_CHECK(hipGetLastError());
     a.order = I.tb_order2.as<uint32_t>();

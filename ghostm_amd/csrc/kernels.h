@@ -2272,15 +2272,21 @@ __global__ __launch_bounds__(256) void k_tb_pairs(const uint32_t *qid, const uin
 
 // Counting-sort scatter: order[prefix(key) + rank] = index, for every index with
 // key > 0 (skip_zero) or every index. hist holds the key counts; cursor (zeroed)
-// hands out the ranks, one global atomic per (block, key).
+// hands out the ranks, one global atomic per (block, key). kCsortItems keys per
+// thread, and the lanes of a wave holding the same key take their ranks with
+// one LDS atomic (ballot matching on the key bits): most keys fall in a few
+// hot bins (windows cut by nothing), whose per-item atomics serialised.
+constexpr uint32_t kCsortItems = 16;
+constexpr uint32_t kCsortTile = 256 * kCsortItems;
 __global__ __launch_bounds__(256) void k_csort_scatter(const uint32_t *key, uint32_t n, bool skip_zero,
                                                        const uint32_t *hist, uint32_t *cursor,
                                                        uint32_t *order) {
+  static_assert(kSortBins == 4 * 256 && kSortBins == 1024, "four bins per thread, ten key bits");
   __shared__ uint32_t s_pre[kSortBins];
   __shared__ uint32_t s_cnt[kSortBins];
   __shared__ uint32_t s_part[256];
   // exclusive prefix of the histogram: 4 bins per thread, then the 256 partials
-  const uint32_t t = threadIdx.x;
+  const uint32_t t = threadIdx.x, lane = t & 63;
   uint32_t v[4], sum = 0;
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
@@ -2304,18 +2310,34 @@ __global__ __launch_bounds__(256) void k_csort_scatter(const uint32_t *key, uint
     run += v[u];
   }
   __syncthreads();
-  const uint32_t k = blockIdx.x * blockDim.x + t;
-  uint32_t b = 0, rank = 0;
-  const bool take = k < n && (!skip_zero || key[k] != 0);
-  if (take) {
-    b = min(key[k], kSortBins - 1);
-    rank = atomicAdd(&s_cnt[b], 1u);
+  const unsigned long long lt = (1ull << lane) - 1;
+  const uint32_t first = blockIdx.x * kCsortTile + t;
+  uint32_t bin[kCsortItems], rank[kCsortItems];
+#pragma unroll
+  for (uint32_t u = 0; u < kCsortItems; ++u) {
+    const uint32_t k = first + u * 256;
+    const bool take = k < n && (!skip_zero || key[k] != 0);
+    const uint32_t b = take ? min(key[k], kSortBins - 1) : 0u;
+    unsigned long long peers = __ballot(take);
+#pragma unroll
+    for (int bit = 0; bit < 10; ++bit) {
+      const unsigned long long bal = __ballot((b >> bit) & 1u);
+      peers &= ((b >> bit) & 1u) ? bal : ~bal;
+    }
+    const uint32_t leader = peers ? (uint32_t)__builtin_ctzll(peers) : lane;
+    uint32_t base = 0;
+    if (take && lane == leader) base = atomicAdd(&s_cnt[b], (uint32_t)__popcll(peers));
+    base = (uint32_t)__shfl((int)base, (int)leader);
+    bin[u] = take ? b : 0xFFFFFFFFu;
+    rank[u] = base + (uint32_t)__popcll(peers & lt);
   }
   __syncthreads();
   for (uint32_t x = t; x < kSortBins; x += blockDim.x)
     if (s_cnt[x]) s_cnt[x] = atomicAdd(&cursor[x], s_cnt[x]);
   __syncthreads();
-  if (take) order[s_pre[b] + s_cnt[b] + rank] = k;
+#pragma unroll
+  for (uint32_t u = 0; u < kCsortItems; ++u)
+    if (bin[u] != 0xFFFFFFFFu) order[s_pre[bin[u]] + s_cnt[bin[u]] + rank[u]] = first + u * 256;
 }
 
 struct TbScanArgs {
