@@ -574,6 +574,7 @@ void Session::DevicePass(QueryData &q, DbData &d, const std::vector<uint32_t> &c
     g0 = g1;
   }
   idle(gb1, ng);
+  TraceMark("cuts", cuts.size());
   std::vector<DeviceModule::ScoreSegment> segs;
   for (const auto &c : cuts) {
     const uint64_t c0 = group_begin(c.first), c1 = c.second < ng ? group_begin(c.second) : c_hi;
@@ -699,6 +700,7 @@ void Session::RunQueryChunk(QueryData &q) {
     stats_.candidates += total;
     TraceMark("seed_done", total);
     const std::vector<Batch> batches = CpuBatches(counts, opt_.max_list_length);
+    TraceMark("batches", batches.size());
     for (size_t bi = 0; bi < batches.size(); ++bi) {
       const Batch &b = batches[bi];
       const uint64_t c0 = offsets[b.q0];
@@ -751,6 +753,7 @@ void Session::RunQueryChunkHostMerge(QueryData &q) {
     const uint64_t total = dev.Seed(q.dev, d.dev, sc, &counts, &offsets);
     stats_.candidates += total;
     const std::vector<Batch> batches = CpuBatches(counts, opt_.max_list_length);
+    TraceMark("batches", batches.size());
     for (const Batch &b : batches) {
       const uint64_t c0 = offsets[b.q0];
       const uint64_t c1 = b.q1 < counts.size() ? offsets[b.q1] : total;

@@ -177,7 +177,11 @@ class DeviceModule {
                  uint32_t base_search_length, int open, int ext, uint32_t *db_start,
                  uint32_t *aln_len, uint32_t *aln_match, float *seq_id);
 
-  DeviceTimes &times() { return times_; }
+  DeviceTimes &times() {
+    SettleSeedTime();
+    return times_;
+  }
+  void SettleSeedTime();
   void ResetTimes() { times_ = DeviceTimes(); }
   void Synchronize();
 

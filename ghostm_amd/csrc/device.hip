@@ -154,7 +154,12 @@ struct DeviceModule::Impl {
   // result lists carried across batches / DB chunks (per group of the query
   // chunk: carry_count[g] SlotHits at carry_hits[g * cap]); DB chunk bases
   DevBuf carry_hits, carry_count, chunk_base;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;          // K1 / K2 launch
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;          // K2 launch (and the synchronous paths)
+  hipEvent_t ev_s0 = nullptr, ev_s1 = nullptr;      // K1: read once the stream has passed them
+  bool seed_pending = false;
+  PinnedBuf h_tasks;                                // a pass's first K2 tasks, uploaded asynchronously
+  std::vector<uint32_t> h_wide;                     // K1 wide-pass query list and group offsets: kept
+  std::vector<unsigned long long> h_wide_goff;      // until the next K1, past their async uploads
   hipEvent_t ev_m0 = nullptr, ev_m1 = nullptr;      // K4
   hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;      // K3
   hipEvent_t ev_done = nullptr, ev_tasks = nullptr; // end of a segment's selection; next tasks uploaded
@@ -225,7 +230,7 @@ void DeviceModule::Bind(int device) {
   stream_ = s;
   copy_stream_ = c;
   for (hipEvent_t *e : {&impl_->ev0, &impl_->ev1, &impl_->ev_m0, &impl_->ev_m1, &impl_->ev_t0, &impl_->ev_t1,
-                        &impl_->ev_done, &impl_->ev_tasks})
+                        &impl_->ev_done, &impl_->ev_tasks, &impl_->ev_s0, &impl_->ev_s1})
     HIP_CHECK(hipEventCreate(e));
   HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_seed<1024, 16384, false>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 16384 * 4));
@@ -403,6 +408,14 @@ static float ElapsedMs(hipEvent_t a, hipEvent_t b) {
   return ms;
 }
 
+// K1's device time, read when something has waited for the stream anyway (the
+// K1 stage itself returns without waiting for its last kernels)
+void DeviceModule::SettleSeedTime() {
+  if (!impl_ || !impl_->seed_pending) return;
+  impl_->seed_pending = false;
+  times_.seed += ElapsedMs(impl_->ev_s0, impl_->ev_s1) * 1e-3;
+}
+
 // K1 size classes: (threads, LDS bins per buffer). Bigger queries get bigger
 // workgroups; the last class merges in global memory.
 struct SeedClass {
@@ -500,7 +513,8 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
   I.offsets.Reserve((size_t)nq * 8);
   I.list_beg.Reserve((size_t)nq * nlists * 4);
   I.list_len.Reserve((size_t)nq * nlists * 4);
-  HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
+  SettleSeedTime();
+  HIP_CHECK(hipEventRecord(I.ev_s0, S(stream_)));
   HIP_CHECK(hipMemsetAsync(I.counts.p, 0, (size_t)nq * 4, S(stream_)));
   TraceMark("k1a_memset");
 
@@ -652,7 +666,8 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
 
   uint64_t total = 0;
   std::vector<uint32_t> wide[4];
-  std::vector<unsigned long long> wide_goff;
+  std::vector<unsigned long long> &wide_goff = I.h_wide_goff;  // outlive the async copies below
+  wide_goff.clear();
   for (uint32_t i = 0; i < nq; ++i) {
     (*offsets)[i] = total;
     total += (*counts)[i];
@@ -682,7 +697,8 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
   for (auto &v : wide) nwide += v.size();
   for (int c = 0; c < 4; ++c) times_.seed_queries_class[c] += cls[c].size();
   times_.seed_queries_wide += nwide;
-  std::vector<uint32_t> all;  // outlives the async copy
+  std::vector<uint32_t> &all = I.h_wide;
+  all.clear();
   if (nwide) {
     all.reserve(nwide);
     for (auto &v : wide) all.insert(all.end(), v.begin(), v.end());
@@ -703,9 +719,9 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
       at += wide[c].size();
     }
   }
-  HIP_CHECK(hipEventRecord(I.ev1, S(stream_)));
+  HIP_CHECK(hipEventRecord(I.ev_s1, S(stream_)));
+  I.seed_pending = true;  // the compaction and wide pass run on while the host cuts batches
   TraceMark("k1c_enq");
-  times_.seed += ElapsedMs(I.ev0, I.ev1) * 1e-3;
   // algorithmic bytes: query record + 2 CSR words per list + one u32 per
   // position + 8 bytes (start, query) per candidate
   times_.seed_bytes += (uint64_t)nq * (q->L + 8ull * nlists) + bins_total * 4ull + total * 8ull;
@@ -715,7 +731,11 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
 void DeviceModule::CopyStarts(uint64_t begin, uint64_t n, uint32_t *out) {
   Use();
   if (n == 0) return;
-  HIP_CHECK(hipMemcpy(out, impl_->cand_start.as<uint32_t>() + begin, n * 4, hipMemcpyDeviceToHost));
+  // the K1 stage returns with its last kernels still queued on stream_
+  HIP_CHECK(hipMemcpyAsync(out, impl_->cand_start.as<uint32_t>() + begin, n * 4, hipMemcpyDeviceToHost,
+                           S(stream_)));
+  HIP_CHECK(hipStreamSynchronize(S(stream_)));
+  SettleSeedTime();
 }
 
 // K2 tasks: runs of <= per_block consecutive candidates spanning <= Qmax queries
@@ -815,11 +835,16 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
   if (buf < 0) {
     std::vector<kern::ScoreTask> tasks;
     BuildScoreTasks(cand_begin, n, q_first, q_end, counts, offsets, per_block, &tasks);
+    TraceMark("tasks", tasks.size());
     buf = I.task_turn;
-    I.task_buf[buf].Reserve(tasks.size() * sizeof(kern::ScoreTask));
-    HIP_CHECK(hipMemcpyAsync(I.task_buf[buf].p, tasks.data(), tasks.size() * sizeof(kern::ScoreTask),
-                             hipMemcpyHostToDevice, S(stream_)));
-    HIP_CHECK(hipStreamSynchronize(S(stream_)));  // the host vector goes out of scope
+    const size_t tb = tasks.size() * sizeof(kern::ScoreTask);
+    I.task_buf[buf].Reserve(tb);
+    // page-locked staging, no wait: the next pass's first segment reuses it
+    // only after this launch has been waited for
+    I.h_tasks.Reserve(tb);
+    if (tb) std::memcpy(I.h_tasks.p, tasks.data(), tb);
+    HIP_CHECK(hipMemcpyAsync(I.task_buf[buf].p, I.h_tasks.p, tb, hipMemcpyHostToDevice, S(stream_)));
+    TraceMark("tasks_up", tasks.size());
     ntasks = tasks.size();
   }
   I.task_turn = 1 - buf;
@@ -922,6 +947,7 @@ void DeviceModule::ScoreFinish() {
   Impl::ScoreState &P = I.score_state;
   if (!P.active) return;
   P.active = false;
+  SettleSeedTime();
   // the counters on the copy stream: the main stream may already hold K4/K3
   unsigned long long cells = 0;
   uint32_t nguard = 0;
