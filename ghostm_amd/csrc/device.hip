@@ -132,7 +132,6 @@ struct DeviceModule::Impl {
     uint32_t count = 0, per_block = 0;
     int buf = 0;
   } prepared;
-  std::vector<kern::ScoreTask> next_tasks;  // host copy of the prepared tasks
   struct ScoreState {                       // the launched, not yet finished K2
     bool active = false, guarded = false;
     uint64_t cand_begin = 0, n = 0;
@@ -157,7 +156,7 @@ struct DeviceModule::Impl {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;          // K2 launch (and the synchronous paths)
   hipEvent_t ev_s0 = nullptr, ev_s1 = nullptr;      // K1: read once the stream has passed them
   bool seed_pending = false;
-  PinnedBuf h_tasks;                                // a pass's first K2 tasks, uploaded asynchronously
+  PinnedBuf h_tasks[2];                             // K2 task staging, one per task buffer
   std::vector<uint32_t> h_wide;                     // K1 wide-pass query list and group offsets: kept
   std::vector<unsigned long long> h_wide_goff;      // until the next K1, past their async uploads
   hipEvent_t ev_m0 = nullptr, ev_m1 = nullptr;      // K4
@@ -738,15 +737,21 @@ void DeviceModule::CopyStarts(uint64_t begin, uint64_t n, uint32_t *out) {
   SettleSeedTime();
 }
 
-// K2 tasks: runs of <= per_block consecutive candidates spanning <= Qmax queries
-static void BuildScoreTasks(uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32_t q_end,
-                            const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets,
-                            uint32_t per_block, std::vector<kern::ScoreTask> *tasks) {
-  tasks->reserve(tasks->size() + n / per_block + (q_end - q_first) / kern::kScoreQmax + 2);
+// K2 tasks: runs of <= per_block consecutive candidates spanning <= Qmax queries,
+// written straight into page-locked staging (no fresh host vector per segment:
+// its first touch cost more than the loop). A task closes when full, when it
+// spans Qmax queries, or at the end, so ScoreTaskBound is an upper bound.
+static size_t ScoreTaskBound(uint64_t n, uint32_t q_first, uint32_t q_end, uint32_t per_block) {
+  return (size_t)(n / per_block) + (q_end - q_first) / kern::kScoreQmax + 2;
+}
+static size_t BuildScoreTasks(uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32_t q_end,
+                              const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets,
+                              uint32_t per_block, kern::ScoreTask *out) {
+  size_t nt = 0;
   kern::ScoreTask cur{};
   bool open_task = false;
   auto flush = [&]() {
-    if (open_task && cur.count) tasks->push_back(cur);
+    if (open_task && cur.count) out[nt++] = cur;
     open_task = false;
   };
   const uint64_t cand_end = cand_begin + n;
@@ -768,6 +773,7 @@ static void BuildScoreTasks(uint64_t cand_begin, uint64_t n, uint32_t q_first, u
     }
   }
   flush();
+  return nt;
 }
 
 // the packed K2 encodings (two candidates per lane) whenever every value fits
@@ -831,21 +837,21 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
     ntasks = I.prepared.count;
     HIP_CHECK(hipStreamWaitEvent(S(stream_), I.ev_tasks, 0));
   }
+  const bool stale = I.prepared.valid;  // an upload nothing will use may still read its staging
   I.prepared.valid = false;
   if (buf < 0) {
-    std::vector<kern::ScoreTask> tasks;
-    BuildScoreTasks(cand_begin, n, q_first, q_end, counts, offsets, per_block, &tasks);
-    TraceMark("tasks", tasks.size());
     buf = I.task_turn;
-    const size_t tb = tasks.size() * sizeof(kern::ScoreTask);
+    if (stale) HIP_CHECK(hipEventSynchronize(I.ev_tasks));
+    // page-locked staging per task buffer: this one's last upload was read by
+    // a launch that has been waited for, so the copy needs no wait either
+    PinnedBuf &hs = I.h_tasks[buf];
+    hs.Reserve(ScoreTaskBound(n, q_first, q_end, per_block) * sizeof(kern::ScoreTask));
+    ntasks = BuildScoreTasks(cand_begin, n, q_first, q_end, counts, offsets, per_block, hs.as<kern::ScoreTask>());
+    TraceMark("tasks", ntasks);
+    const size_t tb = ntasks * sizeof(kern::ScoreTask);
     I.task_buf[buf].Reserve(tb);
-    // page-locked staging, no wait: the next pass's first segment reuses it
-    // only after this launch has been waited for
-    I.h_tasks.Reserve(tb);
-    if (tb) std::memcpy(I.h_tasks.p, tasks.data(), tb);
-    HIP_CHECK(hipMemcpyAsync(I.task_buf[buf].p, I.h_tasks.p, tb, hipMemcpyHostToDevice, S(stream_)));
-    TraceMark("tasks_up", tasks.size());
-    ntasks = tasks.size();
+    HIP_CHECK(hipMemcpyAsync(I.task_buf[buf].p, hs.p, tb, hipMemcpyHostToDevice, S(stream_)));
+    TraceMark("tasks_up", ntasks);
   }
   I.task_turn = 1 - buf;
   I.score_out.Reserve(n * 4);
@@ -927,15 +933,16 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
   // the copy stream into the other buffer (its last reader, the previous K2,
   // has finished: ScoreFinish waited for it)
   if (next && next->n) {
-    std::vector<kern::ScoreTask> &nt = I.next_tasks;
-    nt.clear();
-    BuildScoreTasks(next->cand_begin, next->n, next->q_first, next->q_end, counts, offsets, per_block, &nt);
     const int nb = I.task_turn;
-    I.task_buf[nb].Reserve(nt.size() * sizeof(kern::ScoreTask));
-    HIP_CHECK(hipMemcpyAsync(I.task_buf[nb].p, nt.data(), nt.size() * sizeof(kern::ScoreTask),
-                             hipMemcpyHostToDevice, S(copy_stream_)));
+    PinnedBuf &hs = I.h_tasks[nb];
+    hs.Reserve(ScoreTaskBound(next->n, next->q_first, next->q_end, per_block) * sizeof(kern::ScoreTask));
+    const size_t nt = BuildScoreTasks(next->cand_begin, next->n, next->q_first, next->q_end, counts, offsets,
+                                      per_block, hs.as<kern::ScoreTask>());
+    I.task_buf[nb].Reserve(nt * sizeof(kern::ScoreTask));
+    HIP_CHECK(hipMemcpyAsync(I.task_buf[nb].p, hs.p, nt * sizeof(kern::ScoreTask), hipMemcpyHostToDevice,
+                             S(copy_stream_)));
     HIP_CHECK(hipEventRecord(I.ev_tasks, S(copy_stream_)));
-    I.prepared = Impl::Prepared{true, next->cand_begin, next->n, (uint32_t)nt.size(), per_block, nb};
+    I.prepared = Impl::Prepared{true, next->cand_begin, next->n, (uint32_t)nt, per_block, nb};
   }
 }
 
