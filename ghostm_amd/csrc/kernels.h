@@ -893,6 +893,12 @@ __device__ inline uint32_t BfiV(uint32_t m, uint32_t x, uint32_t y) {  // (x & m
   asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(x), "v"(y));
   return r;
 }
+// the same with y wave-uniform, read straight from an SGPR (no v_mov)
+__device__ inline uint32_t BfiVS(uint32_t m, uint32_t x, uint32_t y) {
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(x), "s"(y));
+  return r;
+}
 __device__ inline uint32_t PkAddU16(uint32_t a, uint32_t b) {
   uint32_t r;
   asm("v_pk_add_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
@@ -1302,11 +1308,14 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
   // col: the step of the last update per half (wave-uniform, an SGPR operand);
   // the lane's column is step - i, taken at the end (starts at column 0)
   uint32_t best = 0, col = (i & 0xFFFFu) * 0x10001u;
-  uint32_t nend = 0;
+  // m: the diagonal mask of the column being computed (0 in halves whose
+  // previous column was END), set by the previous column; any_prev: some lane
+  // of the wave met END in the previous column
+  uint32_t mreg = C::kOne;
+  bool any_prev = false;
   // what the lane below reads before this lane's first column: real 0 in its
   // frame for H (sigma(-i - 1)), and a real F below 0
   uint32_t hout = sig_prev, fout = NEGF, hprev = sig_prev;
-  uint32_t prev_end = 0;
   uint32_t c0A = dbp[xA], c0B = dbp[xB], c1A = dbp[xA + 1], c1B = dbp[xB + 1];
   const uint32_t steps = a.base + a.G - 1;
   const uint32_t wA_ = vA ? wA : 0u, wB_ = vB ? wB : 0u;
@@ -1337,12 +1346,14 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
     const uint32_t rr = rA | (rB << 16);
     uint32_t end = PkSign(PkAddU16(rr, 0x7FE77FE7u));  // codes >= 25
     if constexpr (in_fill) end &= ~fillm;
-    const hf2 m = HF(C::kOne & ~prev_end);
-    prev_end = end;
-    // the next column's frame: one step on, or restarted at 0 after a true END;
-    // E needs the explicit reset only where the half already met one
-    const uint32_t reset = end & seen;
-    seen |= end;
+    const hf2 m = HF(mreg);
+    // quiet: no lane of the wave meets END in this column or the one before
+    // (most columns), so m is kOne, the frame steps on, nothing resets and
+    // the best update needs no END term (a wave-uniform branch)
+    const bool any_end = __builtin_amdgcn_ballot_w64(end != 0) != 0;
+    const bool quiet = !tested && !any_end && !any_prev;
+    any_prev = any_end;
+    // the next column's frame: one step on, or restarted at 0 after a true END
     const uint32_t zn = BfiV(end, EXTP, W(HF(sig) + HF(EXTP)));
     const hf2 Z1 = HF(zn);
     lds_u4 *pA = (lds_u4 *)(uintptr_t)MadU24s(rA, RS2, baseA2);
@@ -1383,17 +1394,30 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
     }
     hout = H[S - 1];
     fout = F;
-    // halves to reset: E restarts at real 0 in the new frame (H needs nothing:
-    // the next column masks the diagonal, and F restarts from the lane above)
-    if (__builtin_amdgcn_ballot_w64(reset != 0)) {  // wave-uniform: a real branch
+    // E is complete here: keeps the compiler from sinking the 32 E updates past
+    // the quiet branch, which holds 32 more values live (136 VGPRs)
 #pragma unroll
-      for (int k = 0; k < S; ++k) E[k] = BfiV(reset, zn, E[k]);
-    }
+    for (int k = 0; k < S; ++k) asm("" : "+v"(E[k]));
     const uint32_t cmr = W(HF(cm) - HF(sig));  // real column maximum (>= 0 off END)
-    const uint32_t keep = PkSign(PkSubI16(cmr, best)) | end | fillm;
-    best = BfiV(keep, best, cmr);
-    col = BfiV(keep, col, step * 0x10001u);
-    nend = PkAddU16(nend, end | fillm);
+    if (quiet) {
+      const uint32_t keep = PkSign(PkSubI16(cmr, best));
+      best = BfiV(keep, best, cmr);
+      col = BfiVS(keep, col, __builtin_amdgcn_readfirstlane(step * 0x10001u));
+    } else {
+      // halves to reset: E restarts at real 0 in the new frame, needed only
+      // where the half already met a true END (H needs nothing: the next column
+      // masks the diagonal, and F restarts from the lane above)
+      const uint32_t reset = end & seen;
+      seen |= end;
+      if (__builtin_amdgcn_ballot_w64(reset != 0)) {  // wave-uniform: a real branch
+#pragma unroll
+        for (int k = 0; k < S; ++k) E[k] = BfiV(reset, zn, E[k]);
+      }
+      const uint32_t keep = PkSign(PkSubI16(cmr, best)) | end | fillm;
+      best = BfiV(keep, best, cmr);
+      col = BfiVS(keep, col, __builtin_amdgcn_readfirstlane(step * 0x10001u));
+      mreg = C::kOne & ~end;
+    }
     sig = zn;
   };
   const uint32_t fill = min(a.G - 1, steps);
@@ -1406,8 +1430,8 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
   }
   for (; step < a.base; ++step) column(step, std::false_type{}, std::false_type{});
   for (; step < steps; ++step) column(step, std::true_type{}, std::false_type{});
-  const uint32_t ncolsA = steps - ((0x10000u - (nend & 0xFFFFu)) & 0xFFFFu);
-  const uint32_t ncolsB = steps - ((0x10000u - (nend >> 16)) & 0xFFFFu);
+  // cells: L x the window's columns (the reference's loop visits END columns too)
+  const uint32_t ncolsA = wA_, ncolsB = wB_;
   int BA = C::Decode(best & 0xFFFFu), CA = (int)(((col & 0xFFFFu) - i) & 0xFFFFu);
   int BB = C::Decode(best >> 16), CB = (int)(((col >> 16) - i) & 0xFFFFu);
   for (uint32_t k = 1; k < a.G; ++k) {
