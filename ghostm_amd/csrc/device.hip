@@ -155,6 +155,8 @@ struct DeviceModule::Impl {
   DevBuf carry_hits, carry_count, chunk_base;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;          // K2 launch (and the synchronous paths)
   hipEvent_t ev_s0 = nullptr, ev_s1 = nullptr;      // K1: read once the stream has passed them
+  hipEvent_t ev_nb = nullptr;                       // K1a's bin counts on the host
+  int seed_early = 1;                               // K1b class launched before the host class pass
   bool seed_pending = false;
   PinnedBuf h_tasks[2];                             // K2 task staging, one per task buffer
   std::vector<uint32_t> h_wide;                     // K1 wide-pass query list and group offsets: kept
@@ -229,7 +231,7 @@ void DeviceModule::Bind(int device) {
   stream_ = s;
   copy_stream_ = c;
   for (hipEvent_t *e : {&impl_->ev0, &impl_->ev1, &impl_->ev_m0, &impl_->ev_m1, &impl_->ev_t0, &impl_->ev_t1,
-                        &impl_->ev_done, &impl_->ev_tasks, &impl_->ev_s0, &impl_->ev_s1})
+                        &impl_->ev_done, &impl_->ev_tasks, &impl_->ev_s0, &impl_->ev_s1, &impl_->ev_nb})
     HIP_CHECK(hipEventCreate(e));
   HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_seed<1024, 16384, false>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 16384 * 4));
@@ -546,8 +548,42 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
     HIP_CHECK(hipMemcpyAsync(nbins_v.data(), I.nelem.p, (size_t)nq * 4, hipMemcpyDeviceToHost, S(stream_)));
     nbins = nbins_v.data();
   }
+  HIP_CHECK(hipEventRecord(I.ev_nb, S(stream_)));
+  // K1b path: the LDS classes count bins in a hash table when every bin + 2 <
+  // 2^21; classes 0 and 1 put the presence filter in front of it when T >= 2
+  // (GHOSTM_K1=merge keeps the merge kernel, =hash the unfiltered table)
+  const char *k1 = getenv("GHOSTM_K1");
+  const bool hash = !(k1 && strcmp(k1, "merge") == 0) && d->len > 0 &&
+                    ((uint64_t)(d->len - 1) >> cfg.log_region) + 2 < kern::kHashBinLimit;
+  const bool filter = hash && cfg.threshold >= 2 && !(k1 && strcmp(k1, "hash") == 0);
+  kern::SeedArgs a{};
+  a.positions = d->pos.as<uint32_t>();
+  a.nlists = nlists;
+  a.shift = cfg.shift;
+  a.log_region = cfg.log_region;
+  a.threshold = cfg.threshold;
+  a.list_beg = I.list_beg.as<uint32_t>();
+  a.list_len = I.list_len.as<uint32_t>();
+  a.counts = I.counts.as<uint32_t>();
+  a.slots = I.slots.as<uint32_t>();
+  a.slot_cap = slot_cap;
+  // the class that held most queries last time is launched now, over every
+  // query (its blocks pick their queries from the device bin counts), so the
+  // GPU works through it while the host sorts the rest into class lists
+  const int n_lds = filter ? 2 : hash ? 3 : 0;  // classes with an identity launch
+  const char *early_env = getenv("GHOSTM_K1_EARLY");
+  int early = early_env && strcmp(early_env, "0") == 0 ? -1 : std::min(I.seed_early, n_lds - 1);
+  if (early >= 0) {
+    kern::SeedArgs b = a;
+    b.query_list = nullptr;
+    b.nbins = I.nelem.as<uint32_t>();
+    b.nb_lo = early == 0 ? 0u : caps[early - 1];
+    b.nb_hi = caps[early];
+    if (filter) LaunchSeedFilterClass(early, b, nq, S(stream_));
+    else LaunchSeedHashClass(early, b, nq, S(stream_));
+  }
   TraceMark("k1a_enq");
-  HIP_CHECK(hipStreamSynchronize(S(stream_)));
+  HIP_CHECK(hipEventSynchronize(I.ev_nb));
   TraceMark("k1a_done");
 
   // size classes (queries without any position keep count 0): one counting
@@ -562,6 +598,8 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
     if (n) ++ncls[class_of(n)];
   }
   const size_t list_total = (size_t)ncls[0] + ncls[1] + ncls[2] + ncls[3];
+  for (int c = 0; c < n_lds; ++c)
+    if (ncls[c] > ncls[I.seed_early < n_lds ? I.seed_early : 0]) I.seed_early = c;
   I.h_qlist.Reserve(list_total * 4 + 4);
   uint32_t *hl = I.h_qlist.as<uint32_t>();
   struct Span {
@@ -597,31 +635,14 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
     HIP_CHECK(hipMemcpyAsync(I.gbuf_off.p, goff.data(), goff.size() * 8, hipMemcpyHostToDevice, S(stream_)));
   }
 
-  kern::SeedArgs a{};
-  a.positions = d->pos.as<uint32_t>();
-  a.nlists = nlists;
-  a.shift = cfg.shift;
-  a.log_region = cfg.log_region;
-  a.threshold = cfg.threshold;
-  a.list_beg = I.list_beg.as<uint32_t>();
-  a.list_len = I.list_len.as<uint32_t>();
-  a.counts = I.counts.as<uint32_t>();
-  a.slots = I.slots.as<uint32_t>();
-  a.slot_cap = slot_cap;
   a.gbuf = I.gbuf.as<uint32_t>();
   a.gbuf_off = I.gbuf_off.as<unsigned long long>();
-  // K1b pass 1: every class, candidates into per-query slots (largest first).
-  // The LDS classes count bins in a hash table when every bin + 2 < 2^21;
-  // classes 0 and 1 put the presence filter in front of it when T >= 2
-  // (GHOSTM_K1=merge keeps the merge kernel, =hash the unfiltered table).
-  const char *k1 = getenv("GHOSTM_K1");
-  const bool hash = !(k1 && strcmp(k1, "merge") == 0) && d->len > 0 &&
-                    ((uint64_t)(d->len - 1) >> cfg.log_region) + 2 < kern::kHashBinLimit;
-  const bool filter = hash && cfg.threshold >= 2 && !(k1 && strcmp(k1, "hash") == 0);
+  // K1b pass 1: every other class, candidates into per-query slots (largest first)
   {
     size_t at = list_total;
     for (int c = 3; c >= 0; --c) {
       at -= cls[c].size();
+      if (c == early) continue;
       kern::SeedArgs b = a;
       b.query_list = I.qlist.as<uint32_t>() + at;
       if (filter && c < 2) LaunchSeedFilterClass(c, b, (uint32_t)cls[c].size(), S(stream_));

@@ -105,7 +105,19 @@ struct SeedArgs {
   uint32_t *out_qid;
   uint32_t *gbuf;                 // global merge buffers (GBUF variant)
   const unsigned long long *gbuf_off;
+  // query_list null: block b serves query b when nb_lo < nbins[b] <= nb_hi (the
+  // class launched before the host has read the bin counts), else returns
+  const uint32_t *nbins;
+  uint32_t nb_lo, nb_hi;
 };
+
+// The query a K1b block serves, or kNoQuery (block-uniform: return at once).
+constexpr uint32_t kNoQuery = 0xFFFFFFFFu;
+__device__ inline uint32_t SeedBlockQuery(const SeedArgs &a) {
+  if (a.query_list) return a.query_list[blockIdx.x];
+  const uint32_t n = a.nbins[blockIdx.x];
+  return n > a.nb_lo && n <= a.nb_hi ? blockIdx.x : kNoQuery;
+}
 
 __device__ inline uint32_t BlockExclusiveScan(uint32_t v, uint32_t *s_part, uint32_t *s_total) {
   const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -500,7 +512,8 @@ __global__ __launch_bounds__(BLOCK) void k_seed_hash(SeedArgs a) {
   static_assert(kPer <= 32 && kPer * BLOCK == TSLOTS && TSLOTS % 8 == 0, "table shape");
   static_assert(kMaxLists <= 256, "list index in a byte");
 
-  const uint32_t q = a.query_list[blockIdx.x];
+  const uint32_t q = SeedBlockQuery(a);
+  if (q == kNoQuery) return;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t nl = a.nlists;
 #pragma unroll
@@ -601,7 +614,8 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   __shared__ uint32_t s_part[kW];
   __shared__ uint32_t s_total, s_qn;
 
-  const uint32_t q = a.query_list[blockIdx.x];
+  const uint32_t q = SeedBlockQuery(a);
+  if (q == kNoQuery) return;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t nl = a.nlists;
   for (uint32_t k = tid; k < kFWords + TSLOTS; k += BLOCK) s_dyn[k] = 0;
