@@ -54,18 +54,22 @@ def _caps(d):
     return ",".join(str(x) for x in q)
 
 
-@pytest.mark.parametrize("k1", ["hash", "merge"])
+@pytest.mark.parametrize("k1", ["hash", "merge", "lists_only"])
 @pytest.mark.parametrize("ds,var,opts", [("syn_small", "default", []), ("syn_dna", "default", []),
                                          ("syn_short", "default", []), ("syn_chunks", "default", []),
                                          ("syn_small", "r4", ["-r", "4"])])
 def test_every_k1_class_and_the_offset_pass(k1, ds, var, opts, dataset, golden):
     """GHOSTM_K1_CAPS lowers the class caps to the dataset's quartiles and
     GHOSTM_K1_SLOT_CAP shrinks the slot to 2 candidates: all four classes and the
-    offset pass for wide queries run, in the hash (default) and merge K1 forms."""
+    offset pass for wide queries run, in the hash (default) and merge K1 forms,
+    and with every class launched from host lists (GHOSTM_K1_EARLY=0: no class
+    launched over all queries before the host class pass)."""
     d = dataset(ds)
     env = {"GHOSTM_K1_CAPS": _caps(d), "GHOSTM_K1_SLOT_CAP": "2"}
     if k1 == "merge":
         env["GHOSTM_K1"] = "merge"
+    if k1 == "lists_only":
+        env["GHOSTM_K1_EARLY"] = "0"
     text, st, hits, dev = _run(d, opts, env)
     assert _sha(text) == golden["aln"][f"{ds}/{var}"]["sha256"]
     for c in range(4):
