@@ -380,7 +380,11 @@ def main() -> None:
         half = packed and per["score_launches_half"] == per["score_launches"]
         peak = PEAK_VALU_PK16_TOPS if packed else PEAK_VALU_TOPS
         framed = half and per.get("score_launches_framed", 0) == per["score_launches"]
-        if framed:
+        swar = framed and per.get("score_launches_swar", 0) == per["score_launches"]
+        if swar:
+            kname = ("k_score16f<32,swar> (K2 Gotoh DP, per-column frame over 16-bit integer patterns: packed "
+                     "f16 max3 on the patterns, v_add_u32 for the constant adds, two candidates per lane)")
+        elif framed:
             kname = ("k_score16f<32> (K2 Gotoh DP, exact integers in packed f16 lanes, per-column frame, "
                      "two candidates per lane)")
         elif half:
@@ -389,7 +393,8 @@ def main() -> None:
             kname = "k_score16<32,int16> (K2 Gotoh DP, packed int16, two candidates per lane)"
         else:
             kname = "k_score (K2 Gotoh DP, int32)"
-        dtype = ("int (exact integers in packed f16 lanes, int16 re-score above the guard)" if half
+        dtype = ("int (exact 16-bit integers; packed f16 max3 orders their patterns, no guard)" if swar
+                 else "int (exact integers in packed f16 lanes, int16 re-score above the guard)" if half
                  else "int16" if packed else "int32")
         pmc = _json(PMC)
         pmc_ok = bool(pmc and pmc.get("queries") == nq and world == 1 and preset == "cfg4" and not args.aln)

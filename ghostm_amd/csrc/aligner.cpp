@@ -1090,6 +1090,7 @@ void Session::Run(bool stream_to_file) {
   stats_.seed_queries_wide = dt.seed_queries_wide;
   stats_.seed_runs_filter = dt.seed_launches_filter;
   stats_.seed_filter_overflows = dt.seed_filter_overflows;
+  stats_.score_launches_swar = dt.score_launches_swar;
   for (size_t k = 0; k < used_parts_; ++k)
     for (const auto &h : parts_[k].hits) stats_.hits += h.size();
 }

@@ -843,9 +843,17 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
   // (the frame before a window's first END starts at -2040 + G * ext_pen)
   const int64_t sigma_max = (int64_t)(base + 2 * lay.G) * (-gap.ext);
   const bool framed = half && sigma_max <= 1000 && !(force && strcmp(force, "f16plain") == 0);
+  // the framed kernel over 16-bit integer patterns (k_score16f<S, true>, the
+  // default): exact with no guard while the largest pattern, the restart value
+  // + the frame + L * max|M| (+ the open step), stays below f16 infinity;
+  // GHOSTM_K2=f16frame keeps the f16-number frame
+  const int64_t swar_low = 1024 + 64 + (-(int64_t)gap.open) + (-(int64_t)gap.ext);
+  const int64_t swar_restart = swar_low + sigma_max + bound + 32;
+  const int64_t swar_top = swar_restart + sigma_max + bound + std::abs((int64_t)gap.open - gap.ext) + 32;
+  const bool swar = framed && swar_top < 0x7C00 && !(force && strcmp(force, "f16frame") == 0);
   // framed: values stay exact and the -2040-based frame stays below the
   // post-END one while best + sigma_max < 2040; beyond, the guard flags them
-  int guard = framed ? (bound + sigma_max < 2040 ? 0 : (int)(2040 - sigma_max)) : (bound < 2048 ? 0 : 2000);
+  int guard = swar ? 0 : framed ? (bound + sigma_max < 2040 ? 0 : (int)(2040 - sigma_max)) : (bound < 2048 ? 0 : 2000);
   if (half && getenv("GHOSTM_K2_GUARD")) guard = atoi(getenv("GHOSTM_K2_GUARD"));  // tests: force re-scores
   const uint32_t per_block = ScorePerBlock(q, base, gap);
   // tasks: prepared for this range by the previous launch (uploaded on the copy
@@ -897,6 +905,8 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
   a.score_out = I.score_out.as<uint32_t>();
   a.end_out = I.end_out.as<uint32_t>();
   a.out_base = cand_begin;
+  a.swar_low = (uint32_t)swar_low;
+  a.swar_restart = (uint32_t)swar_restart;
   // counters: [0] cells (u64), [2] guard count (u32)
   I.counters.Reserve(32);
   HIP_CHECK(hipMemsetAsync(I.counters.p, 0, 32, S(stream_)));
@@ -915,17 +925,20 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
   if (packed) {
     switch (lay.S) {
       case 32:
-        if (framed) hipLaunchKernelGGL((kern::k_score16f<32>), grid, block, lds, S(stream_), a);
+        if (swar) hipLaunchKernelGGL((kern::k_score16f<32, true>), grid, block, lds, S(stream_), a);
+        else if (framed) hipLaunchKernelGGL((kern::k_score16f<32>), grid, block, lds, S(stream_), a);
         else if (half) hipLaunchKernelGGL((kern::k_score16<32, true>), grid, block, lds, S(stream_), a);
         else hipLaunchKernelGGL((kern::k_score16<32, false>), grid, block, lds, S(stream_), a);
         break;
       case 16:
-        if (framed) hipLaunchKernelGGL((kern::k_score16f<16>), grid, block, lds, S(stream_), a);
+        if (swar) hipLaunchKernelGGL((kern::k_score16f<16, true>), grid, block, lds, S(stream_), a);
+        else if (framed) hipLaunchKernelGGL((kern::k_score16f<16>), grid, block, lds, S(stream_), a);
         else if (half) hipLaunchKernelGGL((kern::k_score16<16, true>), grid, block, lds, S(stream_), a);
         else hipLaunchKernelGGL((kern::k_score16<16, false>), grid, block, lds, S(stream_), a);
         break;
       default:
-        if (framed) hipLaunchKernelGGL((kern::k_score16f<8>), grid, block, lds, S(stream_), a);
+        if (swar) hipLaunchKernelGGL((kern::k_score16f<8, true>), grid, block, lds, S(stream_), a);
+        else if (framed) hipLaunchKernelGGL((kern::k_score16f<8>), grid, block, lds, S(stream_), a);
         else if (half) hipLaunchKernelGGL((kern::k_score16<8, true>), grid, block, lds, S(stream_), a);
         else hipLaunchKernelGGL((kern::k_score16<8, false>), grid, block, lds, S(stream_), a);
         break;
@@ -943,6 +956,7 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
   times_.score_launches_packed += packed ? 1 : 0;
   times_.score_launches_half += half ? 1 : 0;
   times_.score_launches_framed += framed ? 1 : 0;
+  times_.score_launches_swar += swar ? 1 : 0;
   P.active = true;
   P.guarded = half && guard;
   P.cand_begin = cand_begin;

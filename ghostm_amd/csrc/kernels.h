@@ -771,6 +771,9 @@ struct ScoreArgs {
   int guard;
   uint32_t *guard_count;
   uint32_t *guard_list;
+  // k_score16f<S, true> (integer patterns): the frame base before a window's
+  // first END and the restart value at every END (host: ScoreSwarFrame)
+  uint32_t swar_low, swar_restart;
 };
 
 template <int S>
@@ -1029,19 +1032,28 @@ __device__ inline uint32_t MulU24(uint32_t a, uint32_t b) {
 // matrix gathers (the element-wise build cost ~5 % of k_score16f's VALU).
 // FRAMED (k_score16f): values carry + ext_pen, row kFillCode is all kNeg16.
 // Padding rows (r < pad) are kNeg16 in every code row.
-template <class C, bool FRAMED>
+// SWAR (k_score16f<S, true>): 16-bit integer patterns instead of f16 numbers.
+// Codes 0..24 carry M + ext_pen as a two's-complement delta, END the absolute
+// restart value (read with m = 0 in the END column itself), every other code
+// and the padding rows a drop that leaves H - drop > 0 far below the frame.
+template <class C, bool FRAMED, bool SWAR = false>
 __device__ __forceinline__ void BuildProfile16(const ScoreArgs &a, const ScoreTask &t, short *s_prof16,
                                                uint32_t RS) {
   short *s_enc = s_prof16 + kScoreQmax * kProfRows16 * RS;
   const int extp = -a.ext;
+  const uint32_t drop = SWAR ? (uint32_t)(0x10000u - (a.swar_low - 64u)) & 0xFFFFu : 0u;
   for (uint32_t e = threadIdx.x; e < 32 * 32; e += kScoreBlock) {
     const uint32_t q = e >> 5, c = e & 31;
     int v = c < 25 ? a.mat[c * 32 + q] : 0;
+    if constexpr (SWAR) {
+      s_enc[e] = (short)(c < kSeqEnd ? (uint32_t)(v + extp) & 0xFFFFu : c == kSeqEnd ? a.swar_restart : drop);
+      continue;
+    }
     if constexpr (FRAMED) v = c == kFillCode ? kNeg16 : v + extp;
     s_enc[e] = C::Encode(v);
   }
   __syncthreads();
-  const uint32_t neg = (uint16_t)C::Encode(kNeg16) * 0x10001u;
+  const uint32_t neg = SWAR ? drop * 0x10001u : (uint16_t)C::Encode(kNeg16) * 0x10001u;
   const uint32_t rows = t.q_count * a.Lpad;
   for (uint32_t p = threadIdx.x; p < rows; p += kScoreBlock) {
     const uint32_t slot = p / a.Lpad, r = p - slot * a.Lpad;
@@ -1050,6 +1062,8 @@ __device__ __forceinline__ void BuildProfile16(const ScoreArgs &a, const ScoreTa
     if (r < a.pad) {
 #pragma unroll
       for (int k = 0; k < 16; ++k) w[k] = neg;
+      if constexpr (SWAR)  // END (code 25, the high half of word 12): the restart, as in real rows
+        w[kSeqEnd >> 1] = (w[kSeqEnd >> 1] & 0xFFFFu) | (a.swar_restart << 16);
     } else {
       const uint32_t q = a.qseq[(size_t)(t.q_first + slot) * a.L + (r - a.pad)];
       const uint4 *src = reinterpret_cast<const uint4 *>(s_enc + q * 32);
@@ -1255,7 +1269,22 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16(ScoreArgs a) {
 // steps where some lane meets END writes E^ = sigma_{j+1} into those halves.
 // Values are exact while every framed value stays below 2048: best + the
 // largest frame (steps * ext_pen); beyond that the guard re-scores in int16.
-template <int S>
+//
+// SWAR = true: the same frame over 16-bit INTEGER patterns. v_pk_maximum3_f16
+// orders non-negative finite f16 patterns like the integers they are, so the
+// three maxima stay one packed op each, while the two constant adds per row
+// pair (oE, F) become one 32-bit v_add_u32 each (VOP2, cheaper to issue than a
+// packed add): both halves hold a value in [swar_low - |open|, 0x7C00) and the
+// constant is the signed pair c * 65536 + c, so no carry crosses the halves.
+// The diagonal term is v_pk_mad_u16 (per half, modulo 2^16). No f16 rounding is
+// involved at all, so no guard: the host runs it when the largest value,
+// swar_restart + frame + L * max|M|, stays below the f16 infinity pattern.
+// END handling moves into the END column itself: its frame restarts at
+// swar_restart (above every value before the window's first END), the diagonal
+// mask m = 0 applies there and the END profile row holds swar_restart, so every
+// row of the END column comes out as real 0 (h = swar_restart; a later END first
+// clears E where the half already met one). The column after it is ordinary.
+template <int S, bool SWAR = false>
 __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
   using C = Cells<true>;
   extern __shared__ __attribute__((aligned(16))) short s_prof16[];
@@ -1263,7 +1292,7 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
   const uint32_t RS = a.Lpad + 8;
   const int extp = -a.ext;
 
-  BuildProfile16<C, true>(a, t, s_prof16, RS);  // row kFillCode: the columns before the window
+  BuildProfile16<C, true, SWAR>(a, t, s_prof16, RS);  // row kFillCode: the columns before the window
   __syncthreads();
 
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1301,9 +1330,14 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
   // the padded DB as a raw buffer (gfx9 descriptor word 3; every access stays
   // inside the padding, so the range is left open)
   const __amdgpu_buffer_rsrc_t dbr = __builtin_amdgcn_make_buffer_rsrc((void *)dbp, 0, 0x7FFFFFFF, 0x00020000);
-  const uint32_t EXTP = C::Pair(extp);
+  // SWAR: per-half integer deltas; KOE32/NEXT32 the signed pairs for v_add_u32
+  const uint32_t EXTP = SWAR ? (uint32_t)extp * 0x10001u : C::Pair(extp);
   const hf2 KOE = HF(C::Pair(a.open - a.ext));
   const hf2 NEXT = HF(C::Pair(a.ext));
+  const uint32_t KOE32 = (uint32_t)((a.open - a.ext) * 65537);
+  const uint32_t NEXT32 = (uint32_t)(a.ext * 65537);
+  const uint32_t ONE = SWAR ? 0x00010001u : C::kOne;
+  const uint32_t RESTART = a.swar_restart * 0x10001u;
 
   // Frame bases: until the window's first true END the frame is based near
   // -2040 (sigma(j) = -2040 + (G + j) * ext_pen), so every value there is
@@ -1312,10 +1346,13 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
   // The fill columns before the window read profile row kFillCode (all
   // kNeg16): the state stays at real 0 through them with no restart, so the
   // frame is one function of the column for every lane of a group.
-  const uint32_t NEGF = C::Pair(-30000);  // F into the first row of a group: real < 0
-  uint32_t sig = C::Pair(-2040 + ((int)a.G - (int)i) * extp);  // sigma(-i), this lane's first column
+  const uint32_t NEGF = SWAR ? 0u : C::Pair(-30000);  // F into the first row of a group: real < 0
+  // sigma(-i), this lane's first column
+  uint32_t sig = SWAR ? (a.swar_low + ((int)a.G - (int)i) * extp) * 0x10001u
+                      : C::Pair(-2040 + ((int)a.G - (int)i) * extp);
   uint32_t H[S], E[S];
-  const uint32_t sig_prev = C::Pair(-2040 + ((int)a.G - (int)i - 1) * extp);
+  const uint32_t sig_prev = SWAR ? (a.swar_low + ((int)a.G - (int)i - 1) * extp) * 0x10001u
+                                 : C::Pair(-2040 + ((int)a.G - (int)i - 1) * extp);
 #pragma unroll
   for (int k = 0; k < S; ++k) { H[k] = sig_prev; E[k] = sig; }
   uint32_t seen = 0;                     // halves past a true END (0xFFFF)
@@ -1325,7 +1362,7 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
   // m: the diagonal mask of the column being computed (0 in halves whose
   // previous column was END), set by the previous column; any_prev: some lane
   // of the wave met END in the previous column
-  uint32_t mreg = C::kOne;
+  uint32_t mreg = ONE;
   bool any_prev = false;
   // what the lane below reads before this lane's first column: real 0 in its
   // frame for H (sigma(-i - 1)), and a real F below 0
@@ -1336,9 +1373,6 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
   auto column = [&](uint32_t step, auto tested_c, auto fill_c) {
     constexpr bool tested = decltype(tested_c)::value, in_fill = decltype(fill_c)::value;
     uint32_t hin = ShiftUp(hout), fin = ShiftUp(fout);
-    if (i == 0) { hin = sig; fin = NEGF; }  // real 0 for H; any real F <= 0 will do
-    const uint32_t diag0 = hprev;
-    hprev = hin;
     uint32_t rA = c0A, rB = c0B;
     uint32_t fillm = 0;  // both halves: this lane's column lies before the window
     if constexpr (tested) {
@@ -1360,19 +1394,46 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
     const uint32_t rr = rA | (rB << 16);
     uint32_t end = PkSign(PkAddU16(rr, 0x7FE77FE7u));  // codes >= 25
     if constexpr (in_fill) end &= ~fillm;
-    const hf2 m = HF(mreg);
-    // quiet: no lane of the wave meets END in this column or the one before
-    // (most columns), so m is kOne, the frame steps on, nothing resets and
-    // the best update needs no END term (a wave-uniform branch)
+    // quiet: no lane of the wave meets END in this column (SWAR) or in this one
+    // or the one before (f16), so m is the unit, the frame steps on, nothing
+    // resets and the best update needs no END term (a wave-uniform branch)
     const bool any_end = __builtin_amdgcn_ballot_w64(end != 0) != 0;
-    const bool quiet = !tested && !any_end && !any_prev;
+    const bool quiet = !tested && !any_end && (SWAR || !any_prev);
     any_prev = any_end;
-    // the next column's frame: one step on, or restarted at 0 after a true END
-    const uint32_t zn = BfiV(end, EXTP, W(HF(sig) + HF(EXTP)));
+    // SWAR: this column's frame (restarted in END halves), its mask, and E
+    // cleared where a half meets a second END, all before the cells
+    uint32_t sigc = sig;
+    if constexpr (SWAR) {
+      mreg = ONE;
+      if (any_end) {
+        sigc = BfiV(end, RESTART, sig);
+        mreg = ONE & ~end;
+        const uint32_t reset = end & seen;
+        seen |= end;
+        if (__builtin_amdgcn_ballot_w64(reset != 0)) {  // wave-uniform: a real branch
+#pragma unroll
+          for (int k = 0; k < S; ++k) E[k] = BfiV(reset, 0u, E[k]);
+        }
+      }
+    }
+    if (i == 0) { hin = sigc; fin = NEGF; }  // real 0 for H; any real F <= 0 will do
+    const uint32_t diag0 = hprev;
+    hprev = hin;
+    const hf2 m = HF(mreg);
+    // the next column's frame: one step on, or (f16) restarted at 0 after a true END
+    const uint32_t zn = SWAR ? sigc + EXTP : BfiV(end, EXTP, W(HF(sig) + HF(EXTP)));
     const hf2 Z1 = HF(zn);
     lds_u4 *pA = (lds_u4 *)(uintptr_t)MadU24s(rA, RS2, baseA2);
     lds_u4 *pB = (lds_u4 *)(uintptr_t)MadU24s(rB, RS2, baseB2);
-    uint32_t diag = diag0, F = fin, cm = sig;
+    uint32_t diag = diag0, F = fin, cm = sigc;
+    auto diag_sum = [&](uint32_t h, uint32_t p) -> uint32_t {
+#ifdef GHOSTM_PROBE_ADD
+      if constexpr (SWAR) return W(U2(h) + U2(p));
+#else
+      if constexpr (SWAR) return W(U2(h) * U2(mreg) + U2(p));  // v_pk_mad_u16
+#endif
+      else return C::Diag(h, m, p);
+    };
 #pragma unroll
     for (int k = 0; k < S; k += 8) {
       const u32x4 qa = pA[k / 8];
@@ -1384,8 +1445,8 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
         return __builtin_amdgcn_perm(wb[u >> 1], wa[u >> 1], (u & 1) ? 0x07060302u : 0x05040100u);
       };
       uint32_t s[8];
-      s[0] = C::Diag(diag, m, prof(0));
-      s[1] = C::Diag(H[k], m, prof(1));
+      s[0] = diag_sum(diag, prof(0));
+      s[1] = diag_sum(H[k], prof(1));
       diag = H[k + 7];
       // row u + 2's perm and diagonal sum and row u's E update sit between the
       // dependent steps h -> oE -> max -> F, so few packed ops read the result
@@ -1396,11 +1457,11 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
         uint32_t p2 = 0;
         if (u + 2 < 8) p2 = prof(u + 2);
         H[k + u] = W(h);
-        const hf2 oE = h + KOE;
-        if (u + 2 < 8) s[u + 2] = C::Diag(H[k + u + 1], m, p2);
+        const hf2 oE = SWAR ? HF(W(h) + KOE32) : h + KOE;
+        if (u + 2 < 8) s[u + 2] = diag_sum(H[k + u + 1], p2);
         const hf2 G = __builtin_elementwise_maximum(HF(F), oE);
         E[k + u] = W(__builtin_elementwise_maximum(__builtin_elementwise_maximum(HF(E[k + u]), oE), Z1));
-        F = W(G + NEXT);
+        F = SWAR ? W(G) + NEXT32 : W(G + NEXT);
       }
       cm = C::Max3(C::Max3(H[k], H[k + 1], H[k + 2]), C::Max3(H[k + 3], H[k + 4], H[k + 5]),
                    C::Max3(H[k + 6], H[k + 7], cm));
@@ -1412,25 +1473,28 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
     // the quiet branch, which holds 32 more values live (136 VGPRs)
 #pragma unroll
     for (int k = 0; k < S; ++k) asm("" : "+v"(E[k]));
-    const uint32_t cmr = W(HF(cm) - HF(sig));  // real column maximum (>= 0 off END)
+    // real column maximum (>= 0 off END)
+    const uint32_t cmr = SWAR ? W(U2(cm) - U2(sigc)) : W(HF(cm) - HF(sig));
     if (quiet) {
       const uint32_t keep = PkSign(PkSubI16(cmr, best));
       best = BfiV(keep, best, cmr);
       col = BfiVS(keep, col, __builtin_amdgcn_readfirstlane(step * 0x10001u));
     } else {
-      // halves to reset: E restarts at real 0 in the new frame, needed only
-      // where the half already met a true END (H needs nothing: the next column
-      // masks the diagonal, and F restarts from the lane above)
-      const uint32_t reset = end & seen;
-      seen |= end;
-      if (__builtin_amdgcn_ballot_w64(reset != 0)) {  // wave-uniform: a real branch
+      if constexpr (!SWAR) {
+        // halves to reset: E restarts at real 0 in the new frame, needed only
+        // where the half already met a true END (H needs nothing: the next column
+        // masks the diagonal, and F restarts from the lane above)
+        const uint32_t reset = end & seen;
+        seen |= end;
+        if (__builtin_amdgcn_ballot_w64(reset != 0)) {  // wave-uniform: a real branch
 #pragma unroll
-        for (int k = 0; k < S; ++k) E[k] = BfiV(reset, zn, E[k]);
+          for (int k = 0; k < S; ++k) E[k] = BfiV(reset, zn, E[k]);
+        }
       }
       const uint32_t keep = PkSign(PkSubI16(cmr, best)) | end | fillm;
       best = BfiV(keep, best, cmr);
       col = BfiVS(keep, col, __builtin_amdgcn_readfirstlane(step * 0x10001u));
-      mreg = C::kOne & ~end;
+      if constexpr (!SWAR) mreg = C::kOne & ~end;
     }
     sig = zn;
   };
@@ -1446,8 +1510,8 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
   for (; step < steps; ++step) column(step, std::true_type{}, std::false_type{});
   // cells: L x the window's columns (the reference's loop visits END columns too)
   const uint32_t ncolsA = wA_, ncolsB = wB_;
-  int BA = C::Decode(best & 0xFFFFu), CA = (int)(((col & 0xFFFFu) - i) & 0xFFFFu);
-  int BB = C::Decode(best >> 16), CB = (int)(((col >> 16) - i) & 0xFFFFu);
+  int BA = SWAR ? (int)(best & 0xFFFFu) : C::Decode(best & 0xFFFFu), CA = (int)(((col & 0xFFFFu) - i) & 0xFFFFu);
+  int BB = SWAR ? (int)(best >> 16) : C::Decode(best >> 16), CB = (int)(((col >> 16) - i) & 0xFFFFu);
   for (uint32_t k = 1; k < a.G; ++k) {
     const int src = (int)(g * a.G + k);
     const int oba = __shfl(BA, src), oca = __shfl(CA, src);

@@ -206,7 +206,7 @@ def test_reference_gpu_batching_rule(dataset):
     lib.FreeGpu()
 
 
-@pytest.mark.parametrize("kind", ["int32", "int16", "f16plain", "k2_nowait", "k3_int32", "k1_merge"])
+@pytest.mark.parametrize("kind", ["int32", "int16", "f16plain", "f16frame", "k2_nowait", "k3_int32", "k1_merge"])
 @pytest.mark.parametrize("ds,var,opts", [("syn_small", "default", []), ("syn_short", "default", []),
                                          ("syn_small", "r64_pam250", ["-r", "64", "-M", cases.PAM250, "-y", "2"])])
 def test_forced_score_encoding_matches_golden(kind, ds, var, opts, dataset, golden, tmp_path):
@@ -229,6 +229,8 @@ def test_forced_score_encoding_matches_golden(kind, ds, var, opts, dataset, gold
         assert st["score_launches_framed"] == st["score_launches"] > 0 and st["score_cells"] > 0
     elif kind == "f16plain":
         assert st["score_launches_half"] == st["score_launches"] > 0 and st["score_launches_framed"] == 0
+    elif kind == "f16frame":  # the f16-number frame (k_score16f<S, false>), guarded where needed
+        assert st["score_launches_framed"] == st["score_launches"] > 0 and st["score_launches_swar"] == 0
     else:
         assert st["score_launches"] > 0 and st["score_launches_half"] == 0
         assert st["score_launches_packed"] == (st["score_launches"] if kind == "int16" else 0)
@@ -238,7 +240,8 @@ def test_default_encoding_is_f16_when_scores_fit(dataset, golden, tmp_path):
     d = dataset("syn_small")
     text, st = _gpu_text(d, [], {}, str(tmp_path / "g.out"))
     assert st["score_launches_half"] == st["score_launches"] > 0
-    assert st["score_launches_framed"] == st["score_launches"]  # k_score16f, the column-framed f16 kernel
+    assert st["score_launches_framed"] == st["score_launches"]  # k_score16f, the column-framed kernel
+    assert st["score_launches_swar"] == st["score_launches"]  # ... over 16-bit integer patterns
     assert st["traceback_launches_key"] == st["traceback_launches"] > 0
     assert st["seed_runs_hash"] > 0
     # PAM250 at L = 127 can reach 2159 > 2047: f16 runs with the re-score guard
