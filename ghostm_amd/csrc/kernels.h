@@ -1427,11 +1427,7 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
     lds_u4 *pB = (lds_u4 *)(uintptr_t)MadU24s(rB, RS2, baseB2);
     uint32_t diag = diag0, F = fin, cm = sigc;
     auto diag_sum = [&](uint32_t h, uint32_t p) -> uint32_t {
-#ifdef GHOSTM_PROBE_ADD
-      if constexpr (SWAR) return W(U2(h) + U2(p));
-#else
       if constexpr (SWAR) return W(U2(h) * U2(mreg) + U2(p));  // v_pk_mad_u16
-#endif
       else return C::Diag(h, m, p);
     };
 #pragma unroll
