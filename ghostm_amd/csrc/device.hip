@@ -259,6 +259,12 @@ void DeviceModule::Bind(int device) {
   GHOSTM_SCAN_ATTR(32, true, true, true) GHOSTM_SCAN_ATTR(32, true, false, true)
   GHOSTM_SCAN_ATTR(16, true, true, true) GHOSTM_SCAN_ATTR(16, true, false, true)
   GHOSTM_SCAN_ATTR(8, true, true, true) GHOSTM_SCAN_ATTR(8, true, false, true)
+#define GHOSTM_SCAN_ATTRW(SS, EE)                                                      \
+  HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_tb_scan<SS, true, EE, true, true>, \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, scan_lds));
+  GHOSTM_SCAN_ATTRW(32, true) GHOSTM_SCAN_ATTRW(32, false) GHOSTM_SCAN_ATTRW(16, true)
+  GHOSTM_SCAN_ATTRW(16, false) GHOSTM_SCAN_ATTRW(8, true) GHOSTM_SCAN_ATTRW(8, false)
+#undef GHOSTM_SCAN_ATTRW
 #undef GHOSTM_SCAN_ATTR2
 #undef GHOSTM_SCAN_ATTR
   {
@@ -1080,6 +1086,13 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
     // must stay exact (GHOSTM_K3_SCAN=f16plain keeps the unframed one)
     const int64_t scan_sigma = (int64_t)(a.base + 2 * lay.G) * (-a.ext);
     const bool framed = half && hmax + scan_sigma < 2048 && !(scan_env && strcmp(scan_env, "f16plain") == 0);
+    // the framed scan over 16-bit integer patterns (the default): exact while
+    // every value stays below the f16 infinity pattern; GHOSTM_K3_SCAN=f16frame
+    // / f16plain / int16 keep the others
+    const int64_t swar_low = 1024 + 64 + (-(int64_t)a.open) + (-(int64_t)a.ext);
+    const bool swar = !(scan_env && (strcmp(scan_env, "f16frame") == 0 || strcmp(scan_env, "f16plain") == 0 ||
+                                     strcmp(scan_env, "int16") == 0)) &&
+                      swar_low + scan_sigma + hmax + std::abs((int64_t)a.open - a.ext) + 64 < 0x7C00;
     const uint32_t NB = kern::kSortBins;
     I.tb_width.Reserve((size_t)n * 4);
     I.tb_ncols.Reserve((size_t)n * 4);
@@ -1146,11 +1159,17 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
     // exact windows (cut at the subject's start) need the DB's subject table
     const bool exact = subj != nullptr;
     sa.best_out = I.tb_best.as<uint32_t>();
+    sa.swar_low = (uint32_t)swar_low;
 #define GHOSTM_SCAN1(SS, HH, EE, FF)                                                                          \
   hipLaunchKernelGGL((kern::k_tb_scan<SS, HH, EE, FF>), dim3(blocks), dim3(kern::kScanBlock), kScanLds, S(stream_), \
                      sa)
+#define GHOSTM_SCANW(SS, EE)                                                                                  \
+  hipLaunchKernelGGL((kern::k_tb_scan<SS, true, EE, true, true>), dim3(blocks), dim3(kern::kScanBlock), kScanLds, \
+                     S(stream_), sa)
 #define GHOSTM_SCAN(SS)                                          \
-  if (framed && exact) GHOSTM_SCAN1(SS, true, true, true);       \
+  if (swar && exact) GHOSTM_SCANW(SS, true);                     \
+  else if (swar) GHOSTM_SCANW(SS, false);                        \
+  else if (framed && exact) GHOSTM_SCAN1(SS, true, true, true);  \
   else if (framed) GHOSTM_SCAN1(SS, true, false, true);          \
   else if (half && exact) GHOSTM_SCAN1(SS, true, true, false);   \
   else if (half) GHOSTM_SCAN1(SS, true, false, false);           \
@@ -1162,6 +1181,7 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
       default: GHOSTM_SCAN(8); break;
     }
 #undef GHOSTM_SCAN
+#undef GHOSTM_SCANW
 #undef GHOSTM_SCAN1
     hipLaunchKernelGGL(kern::k_csort_scatter, gsort, b256, 0, S(stream_), I.tb_ncols.as<uint32_t>(), n, false,
                        hist2, cur2, I.tb_order2.as<uint32_t>());
@@ -1171,6 +1191,7 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
     a.best_h = I.tb_best.as<uint32_t>();
     a.rcodes = q->rcodes.as<uint32_t>();  // built for this Lpad just above
     times_.traceback_launches_scan += 1;
+    times_.traceback_launches_scan_swar += swar ? 1 : 0;
   }
   const uint32_t per_block = (kern::kTbBlock / 64) * lay.gpw;
   const dim3 grid((n + per_block - 1) / per_block), block(kern::kTbBlock);

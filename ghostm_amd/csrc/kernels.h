@@ -2455,6 +2455,7 @@ struct TbScanArgs {
   uint32_t *best_out;          // per slot: the reverse DP's maximum
   uint32_t *hist;              // histogram of ncols (kSortBins)
   unsigned long long *cells;   // += L x scanned columns
+  uint32_t swar_low;           // SWAR: the frame base (integer patterns, as K2's)
 };
 
 // Per query, the table byte offsets (code * 4) of its rows in the reverse DP's
@@ -2483,10 +2484,17 @@ __global__ void k_rev_codes(const uint8_t *qseq, uint32_t nq, uint32_t L, uint32
 // are never read, and the fill columns before the window (END-coded) read an
 // all-kNeg row, which keeps the state at real 0 with no reset. No END penalty
 // switching, no diagonal mask: 6 packed ops per row pair instead of 7.
-template <int S, bool HALF, bool EXACT, bool FRAMED = false>
+// SWAR (with FRAMED): the frame over 16-bit integer patterns as in
+// k_score16f<S, true>, based at swar_low. The table words are signed pairs
+// vb * 65536 + va, so the diagonal sum is one v_add_u32 over both halves like
+// the oE and F steps: three of the six packed ops per row pair become VOP2 adds
+// (every value, dead halves included, stays in [64, 0x7C00): no carry crosses
+// the halves, and the packed f16 maxima order the patterns as integers).
+template <int S, bool HALF, bool EXACT, bool FRAMED = false, bool SWAR = false>
 __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
   using C = Cells<HALF>;
   static_assert(!FRAMED || HALF, "the frame is an f16 kernel");
+  static_assert(!SWAR || FRAMED, "integer patterns: the framed kernel");
   extern __shared__ __attribute__((aligned(16))) uint32_t s_pair[];
   uint32_t *s_hist = s_pair + kPairWords;
   const int extp = -a.ext;
@@ -2496,10 +2504,14 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
     int va = q == kPadCode ? kNeg16 : (ca < 25 && q < 25 ? a.mat[ca * 32 + q] : 0);
     int vb = q == kPadCode ? kNeg16 : (cb < 25 && q < 25 ? a.mat[cb * 32 + q] : 0);
     if constexpr (FRAMED) {
-      va = (q == kPadCode || ca == kSeqEnd) ? kNeg16 : va + extp;
-      vb = (q == kPadCode || cb == kSeqEnd) ? kNeg16 : vb + extp;
+      const int neg = SWAR ? 64 - (int)a.swar_low : (int)kNeg16;
+      va = (q == kPadCode || ca == kSeqEnd) ? neg : va + extp;
+      vb = (q == kPadCode || cb == kSeqEnd) ? neg : vb + extp;
     }
-    s_pair[e] = (uint32_t)(unsigned short)C::Encode(va) | (uint32_t)(unsigned short)C::Encode(vb) << 16;
+    if constexpr (SWAR)
+      s_pair[e] = (uint32_t)(vb * 65536 + va);
+    else
+      s_pair[e] = (uint32_t)(unsigned short)C::Encode(va) | (uint32_t)(unsigned short)C::Encode(vb) << 16;
   }
   for (uint32_t b = threadIdx.x; b < kSortBins; b += kScanBlock) s_hist[b] = 0;
   __syncthreads();
@@ -2546,9 +2558,14 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
     }
     uint32_t H[S], E[S];
     // FRAMED: sigma(j) = (G + j) * ext_pen, this lane starts at column -i
-    const uint32_t EXTP = Cells<true>::Pair(extp);
-    uint32_t sig = FRAMED ? Cells<true>::Pair(((int)a.G - (int)i) * extp) : 0u;
-    const uint32_t sig_prev = FRAMED ? Cells<true>::Pair(((int)a.G - (int)i - 1) * extp) : 0u;
+    const uint32_t EXTP = SWAR ? (uint32_t)extp * 0x10001u : Cells<true>::Pair(extp);
+    uint32_t sig = SWAR     ? (a.swar_low + ((int)a.G - (int)i) * extp) * 0x10001u
+                   : FRAMED ? Cells<true>::Pair(((int)a.G - (int)i) * extp)
+                            : 0u;
+    const uint32_t sig_prev = SWAR     ? (a.swar_low + ((int)a.G - (int)i - 1) * extp) * 0x10001u
+                              : FRAMED ? Cells<true>::Pair(((int)a.G - (int)i - 1) * extp)
+                                       : 0u;
+    const uint32_t KOE32 = (uint32_t)((a.open - a.ext) * 65537), NEXT32 = (uint32_t)(a.ext * 65537);
 #pragma unroll
     for (int k = 0; k < S; ++k) { H[k] = sig_prev; E[k] = sig; }
     uint32_t best = 0, col = 0;                 // packed halves
@@ -2604,7 +2621,7 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
           prev_end = end;
         }
       }
-      const hf2 Z1 = HF(W(HF(sig) + HF(EXTP)));  // FRAMED: the next column's frame
+      const hf2 Z1 = SWAR ? HF(sig + EXTP) : HF(W(HF(sig) + HF(EXTP)));  // FRAMED: the next column's frame
       const hf2 KOE = HF(Cells<true>::Pair(a.open - a.ext)), NEXT = HF(Cells<true>::Pair(a.ext));
       const uint32_t cbase = MadU24(min(rA, kPairCodes - 1), kPairCodes * kPairStride * 4,
                                     MulU24(min(rB, kPairCodes - 1), kPairStride * 4));
@@ -2621,7 +2638,11 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
         uint32_t t[CH], tn[CH];
 #pragma unroll
         for (int u = 0; u < CH; ++u) t[u] = T(u);
-        uint32_t sc = W(HF(diag) + HF(t[0]));
+        auto dsum = [](uint32_t h, uint32_t tv) -> uint32_t {
+          if constexpr (SWAR) return h + tv;  // v_add_u32 over both halves
+          else return W(HF(h) + HF(tv));
+        };
+        uint32_t sc = dsum(diag, t[0]);
 #pragma unroll
         for (int k = 0; k < S; k += CH) {
           if (k + CH < S) {
@@ -2631,14 +2652,14 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
 #pragma unroll
           for (int u = 0; u < CH; ++u) {
             uint32_t sn = 0;
-            if (u < CH - 1) sn = W(HF(H[k + u]) + HF(t[u + 1]));
-            else if (k + CH < S) sn = W(HF(H[k + u]) + HF(tn[0]));
+            if (u < CH - 1) sn = dsum(H[k + u], t[u + 1]);
+            else if (k + CH < S) sn = dsum(H[k + u], tn[0]);
             const hf2 h = __builtin_elementwise_maximum(__builtin_elementwise_maximum(HF(sc), HF(E[k + u])), HF(F));
             H[k + u] = W(h);
-            const hf2 oE = h + KOE;
+            const hf2 oE = SWAR ? HF(W(h) + KOE32) : h + KOE;
             const hf2 G = __builtin_elementwise_maximum(HF(F), oE);
             E[k + u] = W(__builtin_elementwise_maximum(__builtin_elementwise_maximum(HF(E[k + u]), oE), Z1));
-            F = W(G + NEXT);
+            F = SWAR ? W(G) + NEXT32 : W(G + NEXT);
             sc = sn;
           }
           cm = C::Max3(C::Max3(H[k], H[k + 1], H[k + 2]), H[k + 3], cm);
@@ -2672,7 +2693,7 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
       // inside the window (j - w < 0) on run steps, else neither END nor dead
       const uint32_t live = run ? PkSign(PkSubI16(jj, ww)) : ~(end | dead);
       if constexpr (FRAMED) {
-        cm = W(HF(cm) - HF(sig));  // real column maximum
+        cm = SWAR ? W(U2(cm) - U2(sig)) : W(HF(cm) - HF(sig));  // real column maximum
         sig = W(Z1);
       }
       const uint32_t upd = PkSign(PkSubI16(best, cm)) & live;
@@ -2687,8 +2708,8 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
     for (; step < general; ++step) column(step, std::false_type{});
     if constexpr (EXACT)
       for (; step < steps; ++step) column(step, std::true_type{});
-    int BA = C::Decode(best & 0xFFFFu), CA = (int)(col & 0xFFFFu);
-    int BB = C::Decode(best >> 16), CB = (int)(col >> 16);
+    int BA = SWAR ? (int)(best & 0xFFFFu) : C::Decode(best & 0xFFFFu), CA = (int)(col & 0xFFFFu);
+    int BB = SWAR ? (int)(best >> 16) : C::Decode(best >> 16), CB = (int)(col >> 16);
     // first column over the group's row strips
     for (uint32_t k = 1; k < a.G; ++k) {
       const int src = (int)(g * a.G + k);

@@ -71,6 +71,7 @@ class GhostmStats(ctypes.Structure):
         ("seed_runs_filter", c_uint64),
         ("seed_filter_overflows", c_uint64),
         ("score_launches_swar", c_uint64),
+        ("traceback_launches_scan_swar", c_uint64),
     ]
 
     def as_dict(self) -> dict:

@@ -199,6 +199,7 @@ typedef struct GhostmStats {
   uint64_t seed_runs_filter;        /* K1 runs whose classes 0/1 used the presence-filtered table */
   uint64_t seed_filter_overflows;   /* ... queries whose filter queue overflowed (redone unfiltered) */
   uint64_t score_launches_swar;     /* framed K2 launches over 16-bit integer patterns (k_score16f<S, true>) */
+  uint64_t traceback_launches_scan_swar; /* K3a scans over 16-bit integer patterns (k_tb_scan<..., true>) */
 } GhostmStats;
 
 /* Session: parse `aln` options exactly like the reference (getopt string
