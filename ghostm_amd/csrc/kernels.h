@@ -1391,13 +1391,25 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
     // offset, no per-column 64-bit address arithmetic
     c1A = __builtin_amdgcn_raw_buffer_load_b8(dbr, xA, step + 2, 0);
     c1B = __builtin_amdgcn_raw_buffer_load_b8(dbr, xB, step + 2, 0);
-    const uint32_t rr = rA | (rB << 16);
-    uint32_t end = PkSign(PkAddU16(rr, 0x7FE77FE7u));  // codes >= 25
-    if constexpr (in_fill) end &= ~fillm;
+    auto end_mask = [&]() {  // 0xFFFF in the END halves (codes >= 25)
+      uint32_t e = PkSign(PkAddU16(rA | (rB << 16), 0x7FE77FE7u));
+      if constexpr (in_fill) e &= ~fillm;
+      return e;
+    };
     // quiet: no lane of the wave meets END in this column (SWAR) or in this one
     // or the one before (f16), so m is the unit, the frame steps on, nothing
-    // resets and the best update needs no END term (a wave-uniform branch)
-    const bool any_end = __builtin_amdgcn_ballot_w64(end != 0) != 0;
+    // resets and the best update needs no END term (a wave-uniform branch).
+    // SWAR on untested steps: the test is one 16-bit max of the two codes, the
+    // END mask is formed only when some lane meets END
+    uint32_t end = 0;
+    bool any_end;
+    if constexpr (SWAR && !tested) {
+      any_end = __builtin_amdgcn_ballot_w64(max((uint16_t)rA, (uint16_t)rB) >= (uint16_t)kSeqEnd) != 0;
+      if (any_end) end = end_mask();
+    } else {
+      end = end_mask();
+      any_end = __builtin_amdgcn_ballot_w64(end != 0) != 0;
+    }
     const bool quiet = !tested && !any_end && (SWAR || !any_prev);
     any_prev = any_end;
     // SWAR: this column's frame (restarted in END halves), its mask, and E
