@@ -173,12 +173,14 @@ struct DeviceModule::Impl {
 };
 
 static constexpr uint32_t kSlotCap = 256;
-// Filtered slot pass (k_seed_filter) of classes 0 and 1, thresholds >= 2:
+// Filtered slot pass (k_seed_filter) of classes 0, 1 and 2, thresholds >= 2:
 // <BLOCK, filter cells, table slots, queue> and its dynamic LDS bytes.
 #define GHOSTM_FILTER0 kern::k_seed_filter<256, 32768, 2304, 1536>
 #define GHOSTM_FILTER1 kern::k_seed_filter<512, 65536, 4608, 3072>
+#define GHOSTM_FILTER2 kern::k_seed_filter<1024, 131072, 9216, 6144>
 constexpr size_t kFilterLds0 = (32768 / 16 + 2304 + 1536) * 4;
 constexpr size_t kFilterLds1 = (65536 / 16 + 4608 + 3072) * 4;
+constexpr size_t kFilterLds2 = (131072 / 16 + 9216 + 6144) * 4;
 
 // K3a: the pair table (32 x 32 codes x 32 query codes, one word each) + histogram
 static constexpr size_t kScanLds = (size_t)kern::kPairWords * 4 + kern::kSortBins * 4;
@@ -249,6 +251,8 @@ void DeviceModule::Bind(int device) {
                                 (int)kFilterLds0));
   HIP_CHECK(hipFuncSetAttribute((const void *)GHOSTM_FILTER1, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)kFilterLds1));
+  HIP_CHECK(hipFuncSetAttribute((const void *)GHOSTM_FILTER2, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)kFilterLds2));
   const int scan_lds = (int)kScanLds;
 #define GHOSTM_SCAN_ATTR(SS, HH, EE, FF)                                             \
   HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_tb_scan<SS, HH, EE, FF>,       \
@@ -464,7 +468,8 @@ static void LaunchSeed(const kern::SeedArgs &a, uint32_t items, hipStream_t s) {
 static void LaunchSeedFilterClass(int cls, const kern::SeedArgs &a, uint32_t items, hipStream_t s) {
   if (items == 0) return;
   if (cls == 0) hipLaunchKernelGGL((GHOSTM_FILTER0), dim3(items), dim3(256), kFilterLds0, s, a);
-  else hipLaunchKernelGGL((GHOSTM_FILTER1), dim3(items), dim3(512), kFilterLds1, s, a);
+  else if (cls == 1) hipLaunchKernelGGL((GHOSTM_FILTER1), dim3(items), dim3(512), kFilterLds1, s, a);
+  else hipLaunchKernelGGL((GHOSTM_FILTER2), dim3(items), dim3(1024), kFilterLds2, s, a);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -556,7 +561,7 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
   }
   HIP_CHECK(hipEventRecord(I.ev_nb, S(stream_)));
   // K1b path: the LDS classes count bins in a hash table when every bin + 2 <
-  // 2^21; classes 0 and 1 put the presence filter in front of it when T >= 2
+  // 2^21; classes 0, 1 and 2 put the presence filter in front of it when T >= 2
   // (GHOSTM_K1=merge keeps the merge kernel, =hash the unfiltered table)
   const char *k1 = getenv("GHOSTM_K1");
   const bool hash = !(k1 && strcmp(k1, "merge") == 0) && d->len > 0 &&
@@ -576,7 +581,7 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
   // the class that held most queries last time is launched now, over every
   // query (its blocks pick their queries from the device bin counts), so the
   // GPU works through it while the host sorts the rest into class lists
-  const int n_lds = filter ? 2 : hash ? 3 : 0;  // classes with an identity launch
+  const int n_lds = hash ? 3 : 0;  // classes with an identity launch
   const char *early_env = getenv("GHOSTM_K1_EARLY");
   int early = early_env && strcmp(early_env, "0") == 0 ? -1 : std::min(I.seed_early, n_lds - 1);
   if (early >= 0) {
@@ -651,7 +656,7 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
       if (c == early) continue;
       kern::SeedArgs b = a;
       b.query_list = I.qlist.as<uint32_t>() + at;
-      if (filter && c < 2) LaunchSeedFilterClass(c, b, (uint32_t)cls[c].size(), S(stream_));
+      if (filter && c < 3) LaunchSeedFilterClass(c, b, (uint32_t)cls[c].size(), S(stream_));
       else if (hash && c < 3) LaunchSeedHashClass(c, b, (uint32_t)cls[c].size(), S(stream_));
       else LaunchSeedClass(c, b, (uint32_t)cls[c].size(), S(stream_));
     }
@@ -670,19 +675,22 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
   TraceMark("k1b_done");
   if (filter) {
     // queries whose filtered queue overflowed: the unfiltered table redoes them
-    std::vector<uint32_t> redo[2];
-    for (int c = 0; c < 2; ++c)
+    std::vector<uint32_t> redo[3];
+    for (int c = 0; c < 3; ++c)
       for (uint32_t qi : cls[c])
         if ((*counts)[qi] == kern::kOverflow) redo[c].push_back(qi);
-    if (!redo[0].empty() || !redo[1].empty()) {
+    if (!redo[0].empty() || !redo[1].empty() || !redo[2].empty()) {
       std::vector<uint32_t> all(redo[0]);
       all.insert(all.end(), redo[1].begin(), redo[1].end());
+      all.insert(all.end(), redo[2].begin(), redo[2].end());
       I.qlist.Reserve(all.size() * 4);
       HIP_CHECK(hipMemcpyAsync(I.qlist.p, all.data(), all.size() * 4, hipMemcpyHostToDevice, S(stream_)));
-      for (int c = 0; c < 2; ++c) {
+      size_t at = 0;
+      for (int c = 0; c < 3; ++c) {
         kern::SeedArgs b = a;
-        b.query_list = I.qlist.as<uint32_t>() + (c ? redo[0].size() : 0);
+        b.query_list = I.qlist.as<uint32_t>() + at;
         LaunchSeedHashClass(c, b, (uint32_t)redo[c].size(), S(stream_));
+        at += redo[c].size();
       }
       HIP_CHECK(hipMemcpyAsync(counts->data(), I.counts.p, (size_t)nq * 4, hipMemcpyDeviceToHost, S(stream_)));
       HIP_CHECK(hipStreamSynchronize(S(stream_)));
