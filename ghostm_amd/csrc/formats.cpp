@@ -56,8 +56,36 @@ static void ReadRaw(std::ifstream &f, T *p, size_t count) {
 
 std::vector<std::string> ReadNameLines(const std::string &path, uint32_t n, bool *complete) {
   std::vector<std::string> names(n);
-  std::ifstream f(path.c_str());
   if (complete) *complete = true;
+  {
+    // the whole file in one read, split at the first n newlines: the same
+    // strings as the getline loop below whenever the file holds n terminated
+    // lines (the usual case); anything shorter takes that loop
+    std::ifstream b(path.c_str(), std::ios::binary);
+    if (!b) return names;
+    b.seekg(0, std::ios::end);
+    const std::streamoff size = b.tellg();
+    if (size > 0) {
+      std::string all((size_t)size, '\0');
+      b.seekg(0);
+      b.read(&all[0], size);
+      if (b.gcount() == size) {
+        std::vector<size_t> ends;
+        ends.reserve(n);
+        for (size_t at = all.find('\n'); at != std::string::npos && ends.size() < n; at = all.find('\n', at + 1))
+          ends.push_back(at);
+        if (ends.size() == n) {
+          size_t from = 0;
+          for (uint32_t i = 0; i < n; ++i) {
+            names[i].assign(all, from, ends[i] - from);
+            from = ends[i] + 1;
+          }
+          return names;
+        }
+      }
+    }
+  }
+  std::ifstream f(path.c_str());
   if (!f) return names;
   uint32_t i = 0;
   std::string line;
