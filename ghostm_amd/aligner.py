@@ -51,16 +51,45 @@ class Aligner:
 class Session:
     """`shard=(rank, world)`: search only that shard of the query set (one process
     per GPU, GhostmSessionCreateShard); rank-order concatenation of the shards'
-    outputs is the unsharded output."""
+    outputs is the unsharded output.
 
-    def __init__(self, argv: Sequence[str], shard: tuple[int, int] | None = None):
+    `exchange`: an all-gather `f(send: bytes, sizes: list[int]) -> bytes` over
+    the ranks (ghostm_amd.shard.torch_allgather): the shard then reads and
+    counts only its own queries, and the ranks agree on the unsharded batch
+    plan through it (GhostmSessionCreateShardEx). Without it, the shard counts
+    every query of the set itself."""
+
+    def __init__(self, argv: Sequence[str], shard: tuple[int, int] | None = None, exchange=None):
         lib = native.load()
         args = ["aln"] + list(argv)
         self._argv = native.argv_array(args)
         if shard is None:
             self._h = lib.GhostmSessionCreate(len(args), self._argv)
-        else:
+        elif exchange is None:
             self._h = lib.GhostmSessionCreateShard(len(args), self._argv, int(shard[0]), int(shard[1]))
+        else:
+            world = int(shard[1])
+            errors = []
+
+            def gather(_ctx, send, nbytes, recv, recv_bytes):
+                try:
+                    sizes = [int(recv_bytes[r]) for r in range(world)]
+                    data = ctypes.string_at(send, nbytes) if nbytes else b""
+                    out = exchange(data, sizes)
+                    if len(out) != sum(sizes):
+                        raise GhostmError(f"all-gather returned {len(out)} bytes, expected {sum(sizes)}")
+                    if out:
+                        ctypes.memmove(recv, out, len(out))
+                    return 0
+                except BaseException as e:  # noqa: BLE001 (reported through the C ABI)
+                    errors.append(e)
+                    return 1
+
+            fn = native.ALLGATHER_FN(gather)  # alive for the duration of the call
+            self._h = lib.GhostmSessionCreateShardEx(len(args), self._argv, int(shard[0]), world,
+                                                     ctypes.cast(fn, ctypes.c_void_p), None)
+            if errors:
+                raise errors[0]
         if not self._h:
             raise GhostmError(native.last_error())
 

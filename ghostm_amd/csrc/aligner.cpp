@@ -3,6 +3,7 @@
 
 #include <fcntl.h>
 #include <getopt.h>
+#include <sched.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -65,9 +66,26 @@ unsigned HostThreads() {
     const int v = atoi(e);
     if (v > 0) return (unsigned)v;
   }
-  unsigned hw = std::thread::hardware_concurrency();
-  if (hw == 0) hw = 1;
-  return std::min(hw, 16u);
+  // the CPUs this process may run on: its affinity mask, capped by a cgroup v2
+  // CPU quota ("<quota> <period>" in cpu.max; "max" = none)
+  unsigned cpus = std::thread::hardware_concurrency();
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  if (sched_getaffinity(0, sizeof(set), &set) == 0) cpus = (unsigned)CPU_COUNT(&set);
+  {
+    std::ifstream f("/sys/fs/cgroup/cpu.max");
+    std::string quota;
+    uint64_t period = 0;
+    if (f >> quota >> period && quota != "max" && period > 0) {
+      const uint64_t q = strtoull(quota.c_str(), nullptr, 10);
+      if (q > 0) cpus = std::min<unsigned>(cpus, (unsigned)std::max<uint64_t>(1, (q + period - 1) / period));
+    }
+  }
+  // shared among the ranks of this node (torchrun sets LOCAL_WORLD_SIZE)
+  unsigned ranks = 1;
+  if (const char *e = getenv("LOCAL_WORLD_SIZE")) ranks = (unsigned)std::max(1, atoi(e));
+  const unsigned share = std::max(1u, cpus) / ranks;
+  return std::max(1u, std::min(share, 16u));
 }
 
 void ParallelFor(size_t n, unsigned threads,
@@ -207,14 +225,6 @@ AlignerOptions ParseAlignerOptions(int argc, char **argv) {
   return o;
 }
 
-// WriteOutput's query length: the index of the last non-X residue + 1, at
-// least 1 (aligner.cpp:959-961); also the query's residue count for the metric
-static uint32_t QueryLength(const uint8_t *s, uint32_t L) {
-  uint32_t e = L - 1;
-  while (e > 0 && s[e] == kBaseX) --e;
-  return e + 1;
-}
-
 // ------------------------------------------------------------------ shards
 void ShardCuts(uint64_t n, const uint32_t *weight, const uint8_t *group_start, uint32_t world, uint64_t *cuts) {
   if (world == 0) throw std::invalid_argument("world must be >= 1");
@@ -232,9 +242,52 @@ void ShardCuts(uint64_t n, const uint32_t *weight, const uint8_t *group_start, u
   cuts[world] = n;
 }
 
-// Keep only this shard's queries: the chunks' queries are cut into `world`
-// contiguous ranges of about equal residues, at name-group starts (groups never
-// span chunks: the reference merges per chunk, aligner.cpp:697-700).
+// The CPU path's batch cuts (aligner.cpp:383-521 driven by Execute's loop at
+// 131-171): a query whose candidates push the running total above -l is carried
+// into the next batch; the loop stops at the first empty batch, so a carried last
+// query is dropped, exactly as the reference does.
+std::vector<Batch> CpuBatches(const std::vector<uint32_t> &counts, uint64_t max_list) {
+  std::vector<Batch> out;
+  const uint32_t n = (uint32_t)counts.size();
+  uint32_t next = 0;
+  int64_t carry = -1;
+  for (;;) {
+    if (next == n) break;
+    uint32_t first = next;
+    uint64_t total = 0;
+    if (carry >= 0) {
+      first = (uint32_t)carry;
+      total = counts[carry];
+    }
+    carry = -1;
+    uint32_t i = next;
+    bool cut = false;
+    for (; i < n; ++i) {
+      total += counts[i];
+      if (total > max_list) { cut = true; break; }
+    }
+    const uint64_t cands = cut ? total - counts[i] : total;
+    const uint32_t stop = cut ? i : n;
+    if (cut) { next = i + 1; carry = i; } else { next = n; }
+    if (cands == 0) break;
+    out.push_back(Batch{first, stop});
+  }
+  return out;
+}
+
+namespace {
+// FNV-1a over a slice's candidate counts: a shard's runs must see the counts
+// its batch plan was made from
+uint64_t CountsHash(const uint32_t *c, size_t n) {
+  uint64_t h = 1469598103934665603ull;
+  for (size_t i = 0; i < n; ++i) {
+    h ^= c[i];
+    h *= 1099511628211ull;
+  }
+  return h;
+}
+}  // namespace
+
 // Name groups (consecutive equal names, merged into one result list:
 // aligner.cpp:697-700) and WriteOutput's query lengths of one query chunk.
 void Session::PrepareQueryChunk(QueryData *qd) {
@@ -251,10 +304,33 @@ void Session::PrepareQueryChunk(QueryData *qd) {
     q.group_last.push_back(q.group_end[i] - 1);
   }
   q.qlen.assign(n, 1);
-  for (uint32_t i = 0; i < n; ++i) q.qlen[i] = QueryLength(&q.chunk.seq[(size_t)i * L], L);
+  for (uint32_t i = 0; i < n; ++i) q.qlen[i] = QueryResidues(&q.chunk.seq[(size_t)i * L], L);
 }
 
+// The batch plan of a slice against DB chunk di, from the counts of its WHOLE
+// chunk: the unsharded run's batches (aligner.cpp:131-171, 511-514), which every
+// shard replays on its own queries (see Passes).
+void Session::PlanFromCounts(QueryData &q, size_t di, const std::vector<uint32_t> &chunk_counts) {
+  if (q.plan.size() <= di) {
+    q.plan.resize(di + 1);
+    q.plan_sum.resize(di + 1);
+    q.plan_hash.resize(di + 1);
+  }
+  q.plan[di] = CpuBatches(chunk_counts, opt_.max_list_length);
+  uint64_t sum = 0;
+  for (uint32_t i = 0; i < q.chunk.nseq; ++i) sum += chunk_counts[q.slice_lo + i];
+  q.plan_sum[di] = sum;
+  q.plan_hash[di] = CountsHash(chunk_counts.data() + q.slice_lo, q.chunk.nseq);
+  q.planned = true;
+}
+
+// Without a collective: the shard counts every query of each chunk it touches
+// itself (K1 on the whole chunk, once), then keeps only its own range. The
+// chunks' queries are cut into `world` contiguous ranges of about equal
+// residues, at name-group starts (groups never span chunks: the reference
+// merges per chunk, aligner.cpp:697-700).
 void Session::ApplyShard(uint32_t rank, uint32_t world) {
+  DeviceModule &dev = DeviceModule::Get();
   std::vector<uint32_t> weight;
   std::vector<uint8_t> start;
   for (const QueryData &q : queries_) {
@@ -269,6 +345,10 @@ void Session::ApplyShard(uint32_t rank, uint32_t world) {
   const uint64_t lo = cuts[rank], hi = cuts[rank + 1];
   shard_begin_ = lo;
   shard_end_ = hi;
+  SeedConfig sc;
+  sc.threshold = opt_.threshold;
+  sc.shift = opt_.shift;
+  sc.log_region = opt_.log_region;
   std::vector<QueryData> kept;
   uint64_t at = 0;  // index of the chunk's first query over the loaded chunks
   for (QueryData &q : queries_) {
@@ -277,6 +357,21 @@ void Session::ApplyShard(uint32_t rank, uint32_t world) {
     const uint64_t b = std::max<uint64_t>(lo, at), e = std::min<uint64_t>(hi, chunk_end);
     if (b < e) {
       const uint32_t i0 = (uint32_t)(b - at), n = (uint32_t)(e - b);
+      // the whole chunk's counts against every DB chunk -> its batch plan
+      q.slice_lo = i0;
+      q.chunk_nseq = c.nseq;
+      DevQuery *full = dev.UploadQuery(c.seq.data(), c.nseq, c.L);
+      std::vector<uint32_t> counts;
+      std::vector<uint64_t> offsets;
+      const uint32_t whole = c.nseq;
+      c.nseq = n;  // PlanFromCounts reads the slice's size
+      for (size_t di = 0; di < dbs_.size(); ++di) {
+        sc.seed_mask = dbs_[di].chunk.seed;
+        dev.Seed(full, dbs_[di].dev, sc, &counts, &offsets);
+        PlanFromCounts(q, di, counts);
+      }
+      c.nseq = whole;
+      dev.Free(full);
       c.seq = std::vector<uint8_t>(c.seq.begin() + (size_t)i0 * c.L, c.seq.begin() + (size_t)(i0 + n) * c.L);
       c.names = std::vector<std::string>(c.names.begin() + i0, c.names.begin() + i0 + n);
       c.nseq = n;
@@ -289,9 +384,120 @@ void Session::ApplyShard(uint32_t rank, uint32_t world) {
   queries_.swap(kept);
 }
 
+// With a collective: every rank has counted its own slices; the ranks
+// all-gather their candidate totals per (query chunk, DB chunk). A chunk whose
+// total fits -l is one batch, as in the unsharded run; otherwise the ranks
+// all-gather the chunk's per-query counts and cut it with the CPU rule.
+// chunk_nseq[c] = queries of chunk c, rank_lo[c][r] = rank r's first query in
+// chunk c (rank_lo[c][world] = chunk_nseq[c]).
+void Session::PlanExchange(uint32_t rank, uint32_t world, const ShardExchange &ex,
+                           const std::vector<uint32_t> &chunk_nseq,
+                           const std::vector<std::vector<uint64_t>> &rank_lo) {
+  DeviceModule &dev = DeviceModule::Get();
+  const size_t nc = chunk_nseq.size(), nd = dbs_.size();
+  SeedConfig sc;
+  sc.threshold = opt_.threshold;
+  sc.shift = opt_.shift;
+  sc.log_region = opt_.log_region;
+  // this rank's counts per (chunk, DB chunk); queries_ holds its slices in chunk order
+  std::vector<QueryData *> slice(nc, nullptr);
+  {
+    size_t k = 0;
+    for (size_t c = 0; c < nc; ++c)
+      if (rank_lo[c][rank] < rank_lo[c][rank + 1]) slice[c] = &queries_.at(k++);
+    if (k != queries_.size()) throw Error("shard slices out of order");
+  }
+  std::vector<std::vector<uint32_t>> mine(nc * nd);
+  std::vector<uint64_t> sums(nc * nd, 0);
+  for (size_t c = 0; c < nc; ++c) {
+    if (!slice[c]) continue;
+    std::vector<uint64_t> offsets;
+    for (size_t di = 0; di < nd; ++di) {
+      sc.seed_mask = dbs_[di].chunk.seed;
+      sums[c * nd + di] = dev.Seed(slice[c]->dev, dbs_[di].dev, sc, &mine[c * nd + di], &offsets);
+    }
+  }
+  auto gather = [&](const void *send, uint64_t bytes, void *recv, const std::vector<uint64_t> &sizes) {
+    if (ex.fn(ex.ctx, send, bytes, recv, sizes.data()) != 0) throw Error("shard exchange (all-gather) failed");
+  };
+  std::vector<uint64_t> all(world * nc * nd);
+  gather(sums.data(), sums.size() * 8, all.data(), std::vector<uint64_t>(world, sums.size() * 8));
+  std::vector<uint64_t> total(nc * nd, 0);
+  for (uint32_t r = 0; r < world; ++r)
+    for (size_t p = 0; p < nc * nd; ++p) total[p] += all[r * nc * nd + p];
+  // pairs that need the whole chunk's counts: more than one batch
+  std::vector<size_t> wide;
+  for (size_t p = 0; p < nc * nd; ++p)
+    if (total[p] > opt_.max_list_length) wide.push_back(p);
+  std::vector<std::vector<uint32_t>> chunk_counts(nc * nd);
+  if (!wide.empty()) {
+    std::vector<uint64_t> sizes(world, 0);
+    for (uint32_t r = 0; r < world; ++r)
+      for (size_t p : wide) sizes[r] += (rank_lo[p / nd][r + 1] - rank_lo[p / nd][r]) * 4;
+    std::vector<uint32_t> send;
+    for (size_t p : wide) send.insert(send.end(), mine[p].begin(), mine[p].end());
+    if (send.size() * 4 != sizes[rank]) throw Error("shard exchange: slice sizes disagree");
+    uint64_t recv_total = 0;
+    for (uint64_t s : sizes) recv_total += s;
+    std::vector<uint32_t> recv(recv_total / 4);
+    gather(send.data(), send.size() * 4, recv.data(), sizes);
+    // rank r's block holds its part of every wide pair in order
+    uint64_t block = 0;
+    for (uint32_t r = 0; r < world; ++r) {
+      uint64_t at = block;
+      for (size_t p : wide) {
+        const uint64_t n = rank_lo[p / nd][r + 1] - rank_lo[p / nd][r];
+        chunk_counts[p].insert(chunk_counts[p].end(), recv.begin() + at, recv.begin() + at + n);
+        at += n;
+      }
+      block += sizes[r] / 4;
+    }
+  }
+  for (size_t c = 0; c < nc; ++c) {
+    QueryData *q = slice[c];
+    if (!q) continue;
+    for (size_t di = 0; di < nd; ++di) {
+      const size_t p = c * nd + di;
+      if (q->plan.size() <= di) {
+        q->plan.resize(di + 1);
+        q->plan_sum.resize(di + 1);
+        q->plan_hash.resize(di + 1);
+      }
+      if (total[p] > opt_.max_list_length) {
+        if (chunk_counts[p].size() != chunk_nseq[c]) throw Error("shard exchange: chunk counts incomplete");
+        q->plan[di] = CpuBatches(chunk_counts[p], opt_.max_list_length);
+      } else if (total[p] > 0) {
+        q->plan[di] = {Batch{0, chunk_nseq[c]}};  // CpuBatches of a chunk within -l
+      } else {
+        q->plan[di].clear();
+      }
+      q->plan_sum[di] = sums[p];
+      q->plan_hash[di] = CountsHash(mine[p].data(), mine[p].size());
+    }
+    q->planned = true;
+  }
+}
+
+std::vector<Batch> Session::Passes(QueryData &q, size_t di, const std::vector<uint32_t> &counts) const {
+  if (!q.planned) return CpuBatches(counts, opt_.max_list_length);
+  uint64_t sum = 0;
+  for (uint32_t c : counts) sum += c;
+  if (di >= q.plan.size() || sum != q.plan_sum[di] || CountsHash(counts.data(), counts.size()) != q.plan_hash[di])
+    throw Error("shard session: candidate counts differ from its batch plan");
+  const uint32_t lo = q.slice_lo, hi = lo + q.chunk.nseq;
+  std::vector<Batch> out;
+  for (const Batch &b : q.plan[di])
+    out.push_back(Batch{std::clamp(b.q0, lo, hi) - lo, std::clamp(b.q1, lo, hi) - lo});
+  return out;
+}
+
 // ------------------------------------------------------------------ session
-Session::Session(const AlignerOptions &opt, uint32_t shard_rank, uint32_t shard_world) : opt_(opt) {
+Session::Session(const AlignerOptions &opt, uint32_t shard_rank, uint32_t shard_world, const ShardExchange *ex)
+    : opt_(opt) {
   threads_ = HostThreads();
+  if (shard_world == 0 || shard_rank >= shard_world) throw std::invalid_argument("shard rank outside the world");
+  shard_world_ = shard_world;
+  const bool local = shard_world > 1 && ex && ex->fn;  // rank-local reads + exchange
   DeviceModule &dev = DeviceModule::Get();
   TraceMark("create");
   dev.Bind(opt_.device);
@@ -319,14 +525,17 @@ Session::Session(const AlignerOptions &opt, uint32_t shard_rank, uint32_t shard_
   DbFile df(opt_.db_prefix);
   const uint32_t nd_chunks = (int64_t)df.division > 0 ? (uint32_t)df.division : 0u;
   std::vector<QueryData> qread(nq_chunks);
+  std::vector<QueryChunkIndex> qidx(local ? nq_chunks : 0);
   std::vector<DbData> dread(nd_chunks);
   std::vector<char> qok(nq_chunks, 0), dok(nd_chunks, 0);
   // (each query chunk's name groups and WriteOutput lengths are derived on its
-  // reading thread too)
+  // reading thread too; a rank-local shard only indexes the query chunks here)
   ParallelFor(nq_chunks + nd_chunks, std::max<unsigned>(1u, std::min(threads_, 8u)),
               [&](size_t b, size_t e, unsigned) {
                 for (size_t k = b; k < e; ++k) {
-                  if (k < nq_chunks) {
+                  if (k < nq_chunks && local) {
+                    qok[k] = qf.IndexChunk(id + (uint32_t)k, &qidx[k]);
+                  } else if (k < nq_chunks) {
                     qok[k] = qf.ReadChunk(id + (uint32_t)k, &qread[k].chunk);
                     if (qok[k]) PrepareQueryChunk(&qread[k]);
                   } else {
@@ -334,15 +543,10 @@ Session::Session(const AlignerOptions &opt, uint32_t shard_rank, uint32_t shard_
                   }
                 }
               });
-  for (uint32_t k = 0; k < nq_chunks && qok[k]; ++k) {
-    qread[k].global_base = base;
-    base += qread[k].chunk.nseq;
-    queries_.push_back(std::move(qread[k]));
-  }
-  if (queries_.empty()) throw std::runtime_error("[Aligner] error: don't find query file.");
-  TraceMark("queries_read", queries_.size());
-  if (shard_world == 0 || shard_rank >= shard_world) throw std::invalid_argument("shard rank outside the world");
-  if (shard_world > 1) ApplyShard(shard_rank, shard_world);  // may leave no queries
+  uint32_t nchunks = 0;
+  while (nchunks < nq_chunks && qok[nchunks]) ++nchunks;
+  if (nchunks == 0) throw std::runtime_error("[Aligner] error: don't find query file.");
+  TraceMark("queries_read", nchunks);
 
   db_sum_u32_ = (uint32_t)df.sum_length;
   uint32_t dbase = 0;
@@ -353,12 +557,6 @@ Session::Session(const AlignerOptions &opt, uint32_t shard_rank, uint32_t shard_
   }
   if (dbs_.empty()) throw std::runtime_error("[Aligner] error: don't find db file.");
   TraceMark("db_read", dbs_.size());
-
-  for (QueryData &q : queries_) {
-    const uint32_t n = q.chunk.nseq, L = q.chunk.L;
-    q.dev = dev.UploadQuery(q.chunk.seq.data(), n, L);
-    dev.SetQueryGroups(q.dev, q.group_first.data(), q.group_last.data(), (uint32_t)q.group_first.size());
-  }
   for (DbData &d : dbs_) {
     const DbChunk &c = d.chunk;
     d.dev = dev.UploadDb(c.seq.data(), c.len, c.keys_count.data(), c.kcl, c.positions.data(), c.npos);
@@ -372,46 +570,69 @@ Session::Session(const AlignerOptions &opt, uint32_t shard_rank, uint32_t shard_
       if (dbs_[k].chunk.id != k) throw Error("DB chunk ids out of order");
     dev.SetChunkBases(bases.data(), (uint32_t)bases.size());
   }
+
+  std::vector<uint32_t> chunk_nseq;
+  std::vector<std::vector<uint64_t>> rank_lo;
+  if (local) {
+    // the cut over every selected query from the chunk indices, then only this
+    // rank's rows and names are read
+    std::vector<uint32_t> weight;
+    std::vector<uint8_t> start;
+    for (uint32_t k = 0; k < nchunks; ++k) {
+      weight.insert(weight.end(), qidx[k].qlen.begin(), qidx[k].qlen.end());
+      start.insert(start.end(), qidx[k].group_start.begin(), qidx[k].group_start.end());
+    }
+    std::vector<uint64_t> cuts(shard_world + 1);
+    ShardCuts(weight.size(), weight.data(), start.data(), shard_world, cuts.data());
+    shard_begin_ = cuts[shard_rank];
+    shard_end_ = cuts[shard_rank + 1];
+    std::vector<uint32_t> read;  // chunks holding queries of this rank
+    uint64_t at = 0;
+    uint32_t cbase = base;
+    chunk_nseq.resize(nchunks);
+    rank_lo.resize(nchunks);
+    for (uint32_t k = 0; k < nchunks; ++k) {
+      const uint32_t n = qidx[k].nseq;
+      chunk_nseq[k] = n;
+      for (uint32_t r = 0; r <= shard_world; ++r)
+        rank_lo[k].push_back(std::min<uint64_t>(n, cuts[r] > at ? cuts[r] - at : 0));
+      if (rank_lo[k][shard_rank] < rank_lo[k][shard_rank + 1]) {
+        qread[k].slice_lo = (uint32_t)rank_lo[k][shard_rank];
+        qread[k].chunk_nseq = n;
+        qread[k].global_base = cbase + qread[k].slice_lo;
+        read.push_back(k);
+      }
+      at += n;
+      cbase += n;
+    }
+    ParallelFor(read.size(), std::max<unsigned>(1u, std::min(threads_, 8u)), [&](size_t b, size_t e, unsigned) {
+      for (size_t j = b; j < e; ++j) {
+        const uint32_t k = read[j];
+        qidx[k].ReadSlice(qread[k].slice_lo, (uint32_t)(rank_lo[k][shard_rank + 1] - qread[k].slice_lo),
+                          &qread[k].chunk);
+        PrepareQueryChunk(&qread[k]);
+      }
+    });
+    for (uint32_t k : read) queries_.push_back(std::move(qread[k]));
+    TraceMark("slices_read", queries_.size());
+  } else {
+    for (uint32_t k = 0; k < nchunks; ++k) {
+      qread[k].global_base = base;
+      base += qread[k].chunk.nseq;
+      queries_.push_back(std::move(qread[k]));
+    }
+    if (shard_world > 1) ApplyShard(shard_rank, shard_world);  // may leave no queries
+  }
+
+  for (QueryData &q : queries_) {
+    const uint32_t n = q.chunk.nseq, L = q.chunk.L;
+    q.dev = dev.UploadQuery(q.chunk.seq.data(), n, L);
+    dev.SetQueryGroups(q.dev, q.group_first.data(), q.group_last.data(), (uint32_t)q.group_first.size());
+  }
+  if (local) PlanExchange(shard_rank, shard_world, *ex, chunk_nseq, rank_lo);
   dev.Synchronize();
   TraceMark("uploaded");
   formatter_.reset(new TaskQueue());
-}
-
-// The CPU path's batch cuts (aligner.cpp:383-521 driven by Execute's loop at
-// 131-171): a query whose candidates push the running total above -l is carried
-// into the next batch; the loop stops at the first empty batch, so a carried last
-// query is dropped, exactly as the reference does.
-struct Batch {
-  uint32_t q0, q1;  // queries [q0, q1)
-};
-
-static std::vector<Batch> CpuBatches(const std::vector<uint32_t> &counts, uint64_t max_list) {
-  std::vector<Batch> out;
-  const uint32_t n = (uint32_t)counts.size();
-  uint32_t next = 0;
-  int64_t carry = -1;
-  for (;;) {
-    if (next == n) break;
-    uint32_t first = next;
-    uint64_t total = 0;
-    if (carry >= 0) {
-      first = (uint32_t)carry;
-      total = counts[carry];
-    }
-    carry = -1;
-    uint32_t i = next;
-    bool cut = false;
-    for (; i < n; ++i) {
-      total += counts[i];
-      if (total > max_list) { cut = true; break; }
-    }
-    const uint64_t cands = cut ? total - counts[i] : total;
-    const uint32_t stop = cut ? i : n;
-    if (cut) { next = i + 1; carry = i; } else { next = n; }
-    if (cands == 0) break;
-    out.push_back(Batch{first, stop});
-  }
-  return out;
 }
 
 namespace {
@@ -699,11 +920,13 @@ void Session::RunQueryChunk(QueryData &q) {
     const uint64_t total = dev.Seed(q.dev, d.dev, sc, &counts, &offsets);
     stats_.candidates += total;
     TraceMark("seed_done", total);
-    const std::vector<Batch> batches = CpuBatches(counts, opt_.max_list_length);
+    // (a shard replays the unsharded run's batches; those that miss its
+    // queries are passes without candidates over its carried lists)
+    const std::vector<Batch> batches = Passes(q, di, counts);
     TraceMark("batches", batches.size());
     for (size_t bi = 0; bi < batches.size(); ++bi) {
       const Batch &b = batches[bi];
-      const uint64_t c0 = offsets[b.q0];
+      const uint64_t c0 = b.q0 < counts.size() ? offsets[b.q0] : total;
       const uint64_t c1 = b.q1 < counts.size() ? offsets[b.q1] : total;
       const bool final_pass = di + 1 == dbs_.size() && bi + 1 == batches.size();
       DevicePass(q, d, counts, offsets, b.q0, b.q1, c0, c1, carry, final_pass);
@@ -748,19 +971,20 @@ void Session::RunQueryChunkHostMerge(QueryData &q) {
   std::vector<uint32_t> score, end;
   Results results(q.chunk.nseq);
   records_on_device_ = false;  // host merge: records are uploaded on demand
-  for (DbData &d : dbs_) {
+  for (size_t di = 0; di < dbs_.size(); ++di) {
+    DbData &d = dbs_[di];
     sc.seed_mask = d.chunk.seed;
     const uint64_t total = dev.Seed(q.dev, d.dev, sc, &counts, &offsets);
     stats_.candidates += total;
-    const std::vector<Batch> batches = CpuBatches(counts, opt_.max_list_length);
+    const std::vector<Batch> batches = Passes(q, di, counts);
     TraceMark("batches", batches.size());
     for (const Batch &b : batches) {
-      const uint64_t c0 = offsets[b.q0];
+      const uint64_t c0 = b.q0 < counts.size() ? offsets[b.q0] : total;
       const uint64_t c1 = b.q1 < counts.size() ? offsets[b.q1] : total;
       const uint64_t nc = c1 - c0;
       score.resize(nc);
       end.resize(nc);
-      dev.Score(q.dev, d.dev, c0, nc, b.q0, b.q1, counts, offsets, base, gap, score.data(), end.data());
+      if (nc) dev.Score(q.dev, d.dev, c0, nc, b.q0, b.q1, counts, offsets, base, gap, score.data(), end.data());
       const double t0 = NowSeconds();
       HostMergeBatch(q, d, b.q0, b.q1, c0, score.data(), end.data(), counts, offsets, &results);
       stats_.seconds_merge += NowSeconds() - t0;
@@ -1025,10 +1249,17 @@ void Session::Run(bool stream_to_file) {
     // an unwritable path writes nothing, as the reference's unchecked ofstream
     stream_fd_ = open(opt_.output_file.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
   }
-  struct CloseStream {  // also on an error: the writer drained, the file closed
+  struct CloseStream {  // also on an error: the formatter, then the writer drained, the file closed
     Session *s;
     ~CloseStream() {
       if (s->stream_fd_ < 0) return;
+      // a formatting task still running may hand a part to the writer, which
+      // must not reach a closed (or reused) descriptor
+      try {
+        s->formatter_->Drain();
+      } catch (...) {
+        s->stream_failed_ = true;
+      }
       try {
         s->writer_->Drain();
       } catch (...) {
@@ -1092,6 +1323,7 @@ void Session::Run(bool stream_to_file) {
   stats_.seed_filter_overflows = dt.seed_filter_overflows;
   stats_.score_launches_swar = dt.score_launches_swar;
   stats_.traceback_launches_scan_swar = dt.traceback_launches_scan_swar;
+  stats_.tracebacks += dt.traced_hits;  // device merge (the host merge counts its own)
   for (size_t k = 0; k < used_parts_; ++k)
     for (const auto &h : parts_[k].hits) stats_.hits += h.size();
 }

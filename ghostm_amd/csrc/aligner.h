@@ -67,8 +67,27 @@ struct HitRecord {
   float seq_id = 0.f;
 };
 
-// Number of host worker threads (GHOSTM_THREADS, default min(16, hardware)).
+// Number of host worker threads: GHOSTM_THREADS, else this process's share of
+// the CPUs it may run on (affinity mask, cgroup quota) divided among the ranks
+// of this node (LOCAL_WORLD_SIZE), between 2 and 16.
 unsigned HostThreads();
+
+// One batch of the reference's batch loop (aligner.cpp:131-171 with
+// SearchNextCpu's cut, :511-514): queries [q0, q1) of a query chunk.
+struct Batch {
+  uint32_t q0, q1;
+};
+
+// The CPU path's batch cuts of one query chunk against one DB chunk, from every
+// query's candidate count.
+std::vector<Batch> CpuBatches(const std::vector<uint32_t> &counts, uint64_t max_list);
+
+// The collective a rank-local shard session uses at creation
+// (GhostmSessionCreateShardEx): an all-gather of byte buffers in rank order.
+struct ShardExchange {
+  GhostmAllGatherFn fn = nullptr;
+  void *ctx = nullptr;
+};
 
 // Parallel for over [0, n) in contiguous blocks.
 void ParallelFor(size_t n, unsigned threads, const std::function<void(size_t, size_t, unsigned)> &fn);
@@ -100,8 +119,13 @@ class Session {
  public:
   // shard_rank/shard_world: search only that shard of the query set (one
   // process per GPU); the shards' outputs concatenated in rank order are the
-  // unsharded output, and hit records keep global query indices.
-  explicit Session(const AlignerOptions &opt, uint32_t shard_rank = 0, uint32_t shard_world = 1);
+  // unsharded output, and hit records keep global query indices. Every shard
+  // replays the unsharded run's batch cuts (the batch plan, fixed here): with
+  // `exchange`, the rank reads and counts only its own queries and the ranks
+  // all-gather their candidate counts; without, the rank counts every query
+  // of the set itself once.
+  explicit Session(const AlignerOptions &opt, uint32_t shard_rank = 0, uint32_t shard_world = 1,
+                   const ShardExchange *exchange = nullptr);
   uint64_t ShardBegin() const { return shard_begin_; }
   uint64_t ShardEnd() const { return shard_end_; }
   ~Session();
@@ -126,6 +150,14 @@ class Session {
     std::vector<uint32_t> group_first, group_last;  // name groups in order
     std::vector<uint32_t> qlen;        // WriteOutput's query length (last non-X + 1)
     uint32_t global_base = 0;          // index of the chunk's first query over all chunks
+    // shard sessions: this slice is queries [slice_lo, slice_lo + nseq) of a
+    // chunk of chunk_nseq queries, and plan[d] holds the whole chunk's batch
+    // cuts against DB chunk d (chunk indices); plan_sum[d] / plan_hash[d] are
+    // the slice's candidate total and count hash, checked on every run
+    bool planned = false;
+    uint32_t slice_lo = 0, chunk_nseq = 0;
+    std::vector<std::vector<Batch>> plan;
+    std::vector<uint64_t> plan_sum, plan_hash;
   };
   struct DbData {
     DbChunk chunk;
@@ -144,6 +176,13 @@ class Session {
 
   static void PrepareQueryChunk(QueryData *q);
   void ApplyShard(uint32_t rank, uint32_t world);
+  // shard sessions: the batch plan of every (query chunk, DB chunk)
+  void PlanFromCounts(QueryData &q, size_t di, const std::vector<uint32_t> &chunk_counts);
+  void PlanExchange(uint32_t rank, uint32_t world, const ShardExchange &ex,
+                    const std::vector<uint32_t> &chunk_nseq, const std::vector<std::vector<uint64_t>> &rank_lo);
+  // the passes of one Seed() result: the plan's batches restricted to the
+  // slice (local indices, possibly empty), or the slice's own cuts unsharded
+  std::vector<Batch> Passes(QueryData &q, size_t di, const std::vector<uint32_t> &counts) const;
   void RunQueryChunk(QueryData &q);
   void RunQueryChunkHostMerge(QueryData &q);
   void DevicePass(QueryData &q, DbData &d, const std::vector<uint32_t> &counts,
@@ -162,6 +201,7 @@ class Session {
 
   AlignerOptions opt_;
   uint64_t shard_begin_ = 0, shard_end_ = UINT64_MAX;  // query range over the loaded chunks
+  uint32_t shard_world_ = 1;
   std::vector<QueryData> queries_;
   std::vector<DbData> dbs_;
   uint32_t db_sum_u32_ = 0;           // DBReader::GetSumDbLength() truncates to u32

@@ -26,15 +26,23 @@ void *GhostmSessionCreate(int argc, char **argv) {
   }
 }
 
-void *GhostmSessionCreateShard(int argc, char **argv, int rank, int world) {
+void *GhostmSessionCreateShardEx(int argc, char **argv, int rank, int world, GhostmAllGatherFn allgather,
+                                 void *ctx) {
   try {
     if (world < 1 || rank < 0 || rank >= world) throw Error("shard rank outside 0..world-1");
     AlignerOptions opt = ParseAlignerOptions(argc, argv);
-    return new Session(opt, (uint32_t)rank, (uint32_t)world);
+    ShardExchange ex;
+    ex.fn = allgather;
+    ex.ctx = ctx;
+    return new Session(opt, (uint32_t)rank, (uint32_t)world, &ex);
   } catch (std::exception &e) {
     SetLastErrorMessage(e.what());
     return nullptr;
   }
+}
+
+void *GhostmSessionCreateShard(int argc, char **argv, int rank, int world) {
+  return GhostmSessionCreateShardEx(argc, argv, rank, world, nullptr, nullptr);
 }
 
 int GhostmSessionShardRange(void *s, uint64_t *begin, uint64_t *end) {

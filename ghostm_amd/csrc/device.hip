@@ -168,7 +168,7 @@ struct DeviceModule::Impl {
   // staging: GHOSTM_K1_PINNED=0 keeps the pageable copies (A/B)
   PinnedBuf h_nbins, h_counts, h_qlist;
   DevBuf counters;     // K2: u64 [0] score cells, u32 at [2] guard count
-  DevBuf tb_counters;  // K3: u64 [0] traceback cells, [1] K3a scan cells
+  DevBuf tb_counters;  // K3: u64 [0] traceback cells, [1] K3a scan cells, [2] hits traced (k_finalize)
   bool matrix_set = false;
 };
 
@@ -1354,8 +1354,8 @@ void DeviceModule::MergeLaunch(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, 
   a.out_start = I.tb_start.as<uint32_t>();
   a.out_ml = I.tb_ml.as<uint32_t>();
   // K3 counters: [0] traceback cells, [1] K3a scan cells
-  I.tb_counters.Reserve(16);
-  HIP_CHECK(hipMemsetAsync(I.tb_counters.p, 0, 16, S(stream_)));
+  I.tb_counters.Reserve(24);
+  HIP_CHECK(hipMemsetAsync(I.tb_counters.p, 0, 24, S(stream_)));
   a.cells = I.tb_counters.as<unsigned long long>();
   HIP_CHECK(hipEventRecord(I.ev_t0, S(stream_)));
   LaunchTraceback(a, q, (uint32_t)slots, d, cap);
@@ -1364,7 +1364,8 @@ void DeviceModule::MergeLaunch(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, 
                      I.sel_count.as<uint32_t>(), I.sel_cand.as<uint32_t>(), I.sel_sid.as<uint32_t>(),
                      I.score_out.as<uint32_t>(), I.end_out.as<uint32_t>(), I.tb_start.as<uint32_t>(),
                      I.tb_ml.as<uint32_t>(), d->subj.as<uint32_t>(), ng, cap, pass.chunk,
-                     m.sel_from, m.carry, I.slot_hits.as<kern::SlotHit>());
+                     m.sel_from, m.carry, I.slot_hits.as<kern::SlotHit>(),
+                     I.tb_counters.as<unsigned long long>() + 2);
   HIP_CHECK(hipGetLastError());
   static_assert(sizeof(kern::SlotHit) == sizeof(SelectedHit), "record layout");
   if (carry_out) {  // the groups' new result lists are the next pass's carry
@@ -1389,7 +1390,7 @@ void DeviceModule::MergeCollect(std::vector<uint32_t> *counts, HostHits *hits) {
   if (hits) *hits = HostHits();
   if (!P.active) return;
   P.active = false;
-  unsigned long long cells[2] = {0, 0};
+  unsigned long long cells[3] = {0, 0, 0};
   HIP_CHECK(hipStreamWaitEvent(S(copy_stream_), I.ev_done, 0));
   HIP_CHECK(hipMemcpyAsync(counts->data(), I.sel_count.p, (size_t)P.ng * 4, hipMemcpyDeviceToHost,
                            S(copy_stream_)));
@@ -1398,12 +1399,13 @@ void DeviceModule::MergeCollect(std::vector<uint32_t> *counts, HostHits *hits) {
     HIP_CHECK(hipMemcpyAsync(hits->data, I.slot_hits.p, P.slots * sizeof(SelectedHit), hipMemcpyDeviceToHost,
                              S(copy_stream_)));
   }
-  HIP_CHECK(hipMemcpyAsync(cells, I.tb_counters.p, 16, hipMemcpyDeviceToHost, S(copy_stream_)));
+  HIP_CHECK(hipMemcpyAsync(cells, I.tb_counters.p, 24, hipMemcpyDeviceToHost, S(copy_stream_)));
   HIP_CHECK(hipStreamSynchronize(S(copy_stream_)));
   times_.merge += ElapsedMs(I.ev_m0, I.ev_m1) * 1e-3;
   times_.traceback += ElapsedMs(I.ev_t0, I.ev_t1) * 1e-3;
   times_.traceback_cells += cells[0];
   times_.traceback_scan_cells += cells[1];
+  times_.traced_hits += cells[2];
 }
 
 void DeviceModule::MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, uint64_t cand_begin, uint64_t n,

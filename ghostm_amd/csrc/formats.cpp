@@ -1,7 +1,14 @@
 // formats.cpp — see formats.h for the layouts and the reference citations.
 #include "formats.h"
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
 #include <climits>
+#include <cstring>
 #include <fstream>
 #include <iostream>
 
@@ -121,6 +128,119 @@ bool QueryFile::ReadChunk(uint32_t id, QueryChunk *q) const {
   std::ifstream s((base + ".seq").c_str(), std::ios::binary);
   if (s) ReadRaw(s, q->seq.data(), q->seq.size());
   return true;
+}
+
+uint32_t QueryResidues(const uint8_t *s, uint32_t L) {
+  uint32_t e = L - 1;
+  while (e > 0 && s[e] == kBaseX) --e;
+  return e + 1;
+}
+
+bool QueryFile::IndexChunk(uint32_t id, QueryChunkIndex *q) const {
+  if (id >= division) return false;
+  q->base = prefix + "_" + std::to_string(id);
+  {
+    std::ifstream f((q->base + ".inf").c_str(), std::ios::binary);
+    if (!f) return false;
+    q->id = id;
+    ReadRaw(f, &q->nseq, 1);
+    ReadRaw(f, &q->L, 1);
+  }
+  const uint32_t n = q->nseq, L = q->L;
+  // residues of every row, from a read-only mapping of the .seq (rows past the
+  // end of a short file are zeros, as ReadChunk leaves them)
+  q->qlen.assign(n, 1);
+  if (L > 0 && n > 0) {
+    const int fd = open((q->base + ".seq").c_str(), O_RDONLY);
+    struct stat st {};
+    const size_t want = (size_t)n * L;
+    size_t have = 0;
+    const uint8_t *map = nullptr;
+    if (fd >= 0 && fstat(fd, &st) == 0 && st.st_size > 0) {
+      have = std::min(want, (size_t)st.st_size);
+      void *m = mmap(nullptr, have, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+      if (m != MAP_FAILED) map = static_cast<const uint8_t *>(m);
+      else have = 0;
+    }
+    std::vector<uint8_t> row(L);
+    for (uint32_t i = 0; i < n; ++i) {
+      const size_t at = (size_t)i * L;
+      if (at + L <= have) {
+        q->qlen[i] = QueryResidues(map + at, L);
+      } else {
+        std::fill(row.begin(), row.end(), 0);
+        if (at < have) std::memcpy(row.data(), map + at, have - at);
+        q->qlen[i] = QueryResidues(row.data(), L);
+      }
+    }
+    if (map) munmap(const_cast<uint8_t *>(map), have);
+    if (fd >= 0) close(fd);
+  }
+  // name lines: the file's bytes and line offsets when it holds n terminated
+  // lines (ReadNameLines' fast case); otherwise every name the reference's way
+  q->nam.clear();
+  q->line.clear();
+  q->names.clear();
+  {
+    std::ifstream b((q->base + ".nam").c_str(), std::ios::binary);
+    if (b) {
+      b.seekg(0, std::ios::end);
+      const std::streamoff size = b.tellg();
+      if (size > 0) {
+        q->nam.resize((size_t)size);
+        b.seekg(0);
+        b.read(&q->nam[0], size);
+        if (b.gcount() != size) q->nam.clear();
+      }
+    }
+    q->line.reserve((size_t)n + 1);
+    q->line.push_back(0);
+    const char *p = q->nam.data(), *e = p + q->nam.size();
+    while (q->line.size() <= n) {
+      const char *nl = static_cast<const char *>(memchr(p, '\n', (size_t)(e - p)));
+      if (!nl) break;
+      q->line.push_back((uint64_t)(nl - q->nam.data()) + 1);
+      p = nl + 1;
+    }
+    if (q->line.size() != (size_t)n + 1) {
+      q->nam.clear();
+      q->line.clear();
+      q->names = ReadNameLines(q->base + ".nam", n, nullptr);
+    }
+  }
+  q->group_start.assign(n, 1);
+  for (uint32_t i = 1; i < n; ++i) {
+    if (!q->names.empty()) {
+      q->group_start[i] = q->names[i] != q->names[i - 1];
+    } else {
+      const uint64_t a0 = q->line[i - 1], a1 = q->line[i] - 1, b0 = q->line[i], b1 = q->line[i + 1] - 1;
+      q->group_start[i] = !(a1 - a0 == b1 - b0 && std::memcmp(&q->nam[a0], &q->nam[b0], a1 - a0) == 0);
+    }
+  }
+  return true;
+}
+
+void QueryChunkIndex::ReadSlice(uint32_t i0, uint32_t n, QueryChunk *q) const {
+  q->id = id;
+  q->nseq = n;
+  q->L = L;
+  q->names.resize(n);
+  for (uint32_t k = 0; k < n; ++k) {
+    const uint32_t i = i0 + k;
+    if (!names.empty()) q->names[k] = names[i];
+    else q->names[k].assign(nam, line[i], line[i + 1] - 1 - line[i]);
+  }
+  q->seq.assign((size_t)n * L, 0);
+  const int fd = open((base + ".seq").c_str(), O_RDONLY);
+  if (fd < 0) return;
+  size_t done = 0;
+  const size_t want = q->seq.size();
+  while (done < want) {
+    const ssize_t r = pread(fd, q->seq.data() + done, want - done, (off_t)((size_t)i0 * L + done));
+    if (r <= 0) break;  // a short file leaves zeros, as ReadChunk
+    done += (size_t)r;
+  }
+  close(fd);
 }
 
 DbFile::DbFile(const std::string &p) : prefix(p) {

@@ -23,12 +23,35 @@ struct QueryChunk {
   std::vector<uint8_t> seq;        // nseq * L codes
 };
 
+// WriteOutput's query length (reference aligner.cpp:959-961): the index of the
+// last non-X code + 1, at least 1; also the query's residues for the metric.
+uint32_t QueryResidues(const uint8_t *row, uint32_t L);
+
+// One query chunk indexed for a rank-local read (multi-GPU shards, SURVEY.md §8
+// e1): every query's residue count from the .seq rows and its name-group start
+// from the .nam lines, without building the names of queries the rank will not
+// search. ReadSlice then reads only the rank's rows and names.
+struct QueryChunkIndex {
+  uint32_t id = 0, nseq = 0, L = 0;
+  std::vector<uint32_t> qlen;          // QueryResidues of every query
+  std::vector<uint8_t> group_start;    // query i's name differs from query i-1's (i = 0: 1)
+  // queries [i0, i0 + n) as ReadChunk would read them (names, codes)
+  void ReadSlice(uint32_t i0, uint32_t n, QueryChunk *out) const;
+
+  std::string base;                    // <prefix>_<id>
+  std::string nam;                     // the .nam file, when it holds nseq terminated lines
+  std::vector<uint64_t> line;          // line k = nam[line[k], line[k + 1] - 1)
+  std::vector<std::string> names;      // otherwise every name, read the reference's way
+};
+
 struct QueryFile {
   std::string prefix;
   uint32_t division = 0, max_length = 0, max_nseq = 0;
   explicit QueryFile(const std::string &prefix);
   // Chunk `id` or false if id >= division / files missing.
   bool ReadChunk(uint32_t id, QueryChunk *out) const;
+  // Index of chunk `id` (see QueryChunkIndex) or false as ReadChunk.
+  bool IndexChunk(uint32_t id, QueryChunkIndex *out) const;
 };
 
 struct DbChunk {

@@ -2229,17 +2229,23 @@ __global__ void k_finalize(const uint32_t *sel_count, const uint32_t *sel_cand,
                            const uint32_t *sel_sid, const uint32_t *score, const uint32_t *end,
                            const uint32_t *tb_start, const uint32_t *tb_ml,
                            const uint32_t *subj_start, uint32_t ng, uint32_t cap, uint32_t chunk,
-                           const uint32_t *sel_from, const SlotHit *carry, SlotHit *out) {
+                           const uint32_t *sel_from, const SlotHit *carry, SlotHit *out,
+                           unsigned long long *traced) {
   const size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= (size_t)ng * cap) return;
-  const uint32_t g = (uint32_t)(s / cap), k = (uint32_t)(s - (size_t)g * cap);
-  if (k >= sel_count[g]) return;
-  if (sel_from && sel_from[s] != kNoSlot) {
-    out[s] = carry[(size_t)g * cap + sel_from[s]];
-    return;
+  bool fresh = false;  // a hit of this pass's candidates, traced back by K3
+  if (s < (size_t)ng * cap) {
+    const uint32_t g = (uint32_t)(s / cap), k = (uint32_t)(s - (size_t)g * cap);
+    if (k < sel_count[g]) {
+      if (sel_from && sel_from[s] != kNoSlot) {
+        out[s] = carry[(size_t)g * cap + sel_from[s]];
+      } else {
+        const uint32_t c = sel_cand[s], sid = sel_sid[s], pos = subj_start[sid];
+        out[s] = SlotHit{sid, score[c], tb_start[s] - pos, end[c] - pos, tb_ml[s], chunk};
+        fresh = true;
+      }
+    }
   }
-  const uint32_t c = sel_cand[s], sid = sel_sid[s], pos = subj_start[sid];
-  out[s] = SlotHit{sid, score[c], tb_start[s] - pos, end[c] - pos, tb_ml[s], chunk};
+  WaveAddCells(traced, fresh ? 1ull : 0ull);
 }
 
 // The gathered hit record (include/ghostm_hip.h GhostmHit), written on the

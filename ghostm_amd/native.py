@@ -20,6 +20,10 @@ HEADER_PATH = os.path.join(REPO_DIR, "include", "ghostm_hip.h")
 
 u32p = POINTER(c_uint32)
 
+# GhostmAllGatherFn (include/ghostm_hip.h): int (*)(void *ctx, const void *send,
+# uint64_t send_bytes, void *recv, const uint64_t *recv_bytes)
+ALLGATHER_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_void_p, c_uint64, c_void_p, POINTER(c_uint64))
+
 
 class GhostmHit(ctypes.Structure):
     """reference Alignment fields gathered per hit (alignment.h:136-145)."""
@@ -111,6 +115,7 @@ SIGNATURES = {
     "GhostmLengthAdjustment": (c_int, [c_float, c_float, c_float, c_float, c_int, c_uint32, c_int, POINTER(c_int)]),
     "GhostmSessionCreate": (c_void_p, [c_int, POINTER(c_char_p)]),
     "GhostmSessionCreateShard": (c_void_p, [c_int, POINTER(c_char_p), c_int, c_int]),
+    "GhostmSessionCreateShardEx": (c_void_p, [c_int, POINTER(c_char_p), c_int, c_int, c_void_p, c_void_p]),
     "GhostmSessionShardRange": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
     "GhostmShardCuts": (c_int, [c_uint64, u32p, POINTER(ctypes.c_uint8), c_int, POINTER(c_uint64)]),
     "GhostmSessionRun": (c_int, [c_void_p]),
@@ -135,6 +140,7 @@ def header_functions(path: str = HEADER_PATH) -> list[str]:
     """Function names declared in include/ghostm_hip.h."""
     text = open(path).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    text = re.sub(r"\btypedef\b[^;]*;", "", text)  # function-pointer types are not exports
     names = re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\(", text)
     skip = {"if", "defined", "sizeof"}
     out = []

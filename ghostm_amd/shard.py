@@ -104,6 +104,29 @@ def gather_bytes(data: bytes, dist, device="cpu") -> list[bytes] | None:
     return [p.cpu().numpy().tobytes() for p in parts]
 
 
+def torch_allgather(dist, device="cpu", group=None):
+    """The all-gather a rank-local shard session needs (Session(exchange=...),
+    GhostmSessionCreateShardEx) over torch.distributed: every rank's byte buffer
+    (sizes[r] bytes from rank r, known to all ranks) concatenated in rank order.
+    Buffers are padded to the largest for one all_gather."""
+    import torch
+
+    def allgather(send: bytes, sizes: list[int]) -> bytes:
+        world = dist.get_world_size(group)
+        if len(sizes) != world:
+            raise ValueError("one size per rank")
+        cap = max(max(sizes), 1)
+        buf = torch.zeros(cap, dtype=torch.uint8)
+        if send:
+            buf[: len(send)] = torch.frombuffer(bytearray(send), dtype=torch.uint8)
+        buf = buf.to(device)
+        parts = [torch.empty_like(buf) for _ in range(world)]
+        dist.all_gather(parts, buf, group=group)
+        return b"".join(p[:n].cpu().numpy().tobytes() for p, n in zip(parts, sizes))
+
+    return allgather
+
+
 def shard_cuts_native(weights, group_start, world: int) -> list[int]:
     """GhostmShardCuts (the C ABI the shard sessions use), for tests."""
     import ctypes

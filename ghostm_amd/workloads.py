@@ -40,6 +40,12 @@ WORKLOADS = {
              "cpu_sample": 4000, "cpu_sample_all": 8000,
              "workload": "cfg5: wide band -r 64, PAM250 11/1, -y 2; synthetic 100k queries x 5M-residue DB"},
 }
+# BASELINE configs[4] is a gap-open/extend sweep: the other seven points of
+# {8, 10, 11, 14} x {1, 2} on the cfg5 data (G11/E1 is "cfg5" itself)
+for _g, _e in ((8, 1), (8, 2), (10, 1), (10, 2), (11, 2), (14, 1), (14, 2)):
+    WORKLOADS[f"cfg5_g{_g}e{_e}"] = dict(
+        WORKLOADS["cfg5"], aln=["-r", "64", "-M", PAM250, "-G", str(_g), "-E", str(_e), "-y", "2"],
+        workload=f"cfg5 gap sweep: -r 64, PAM250 {_g}/{_e}, -y 2; synthetic 100k queries x 5M-residue DB")
 
 
 def _run(exe: str, *args: str) -> None:

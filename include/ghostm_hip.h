@@ -175,8 +175,9 @@ typedef struct GhostmStats {
   uint64_t queries;
   uint64_t query_residues;   /* sum over queries of non-X prefix length */
   uint64_t candidates;
-  uint64_t score_cells;      /* sum over candidates of L x non-END window columns */
-  uint64_t tracebacks;
+  uint64_t score_cells;      /* sum over candidates of L x window columns W (END columns included: the
+                                reference's CalculateScore loop visits them, aligner.cpp:576-660) */
+  uint64_t tracebacks;       /* hits traced back (K3), new selections only */
   uint64_t traceback_cells;
   uint64_t hits;
   uint64_t batches;
@@ -215,10 +216,38 @@ void *GhostmSessionCreate(int argc, char **argv);
  * merges a group into one result list, aligner.cpp:697-700), and this session
  * searches range `rank` on the device given by -D. Hit records keep global
  * query indices, and the shards' outputs concatenated in rank order are the
- * unsharded output byte for byte; the single collective is the caller's gather
- * of GhostmSessionDeviceHits records (RCCL over xGMI). Returns NULL on error.
- * world = 1 is GhostmSessionCreate. */
+ * unsharded output byte for byte; the data-path collective is the caller's
+ * gather of GhostmSessionDeviceHits records (RCCL over xGMI). Returns NULL on
+ * error. world = 1 is GhostmSessionCreate.
+ *
+ * Batch cuts: the reference's output depends on where its batch loop cuts a
+ * query chunk (aligner.cpp:131-171, 511-514: carried result lists are re-sorted
+ * every batch, a batch may split a name group, a chunk whose first query alone
+ * exceeds -l ends early). A shard therefore replays the UNSHARDED run's batches
+ * on its own queries (a batch that misses them is a pass over its carried
+ * lists only). This batch plan is made at creation from the whole chunk's
+ * candidate counts: GhostmSessionCreateShard reads every query of the set and
+ * counts them all itself (K1 once, no communication); see
+ * GhostmSessionCreateShardEx for the rank-local form. Every run re-derives its
+ * counts and fails if they differ from the plan's. */
 void *GhostmSessionCreateShard(int argc, char **argv, int rank, int world);
+
+/* The collective GhostmSessionCreateShardEx calls (on the creating thread, the
+ * same calls in the same order on every rank): an all-gather. Each rank passes
+ * send_bytes bytes; recv receives every rank's buffer concatenated in rank
+ * order, recv_bytes[r] bytes from rank r (known to all ranks). 0 = success. */
+typedef int (*GhostmAllGatherFn)(void *ctx, const void *send, uint64_t send_bytes, void *recv,
+                                 const uint64_t *recv_bytes);
+
+/* GhostmSessionCreateShard for one process per GPU with a communicator: the
+ * rank reads only the .seq rows and .nam lines of its own range (every rank
+ * still derives the cut from all queries' residue counts and name-group
+ * starts), counts only its own queries, and the ranks agree on the batch plan
+ * with one all-gather of their candidate totals per (query chunk, DB chunk),
+ * plus one of the per-query counts when some chunk needs more than one batch.
+ * allgather == NULL is GhostmSessionCreateShard. */
+void *GhostmSessionCreateShardEx(int argc, char **argv, int rank, int world, GhostmAllGatherFn allgather,
+                                 void *ctx);
 
 /* The query range [begin, end) of a shard session, as indices over the
  * selected chunks' queries (0, UINT64_MAX for an unsharded session). */

@@ -183,7 +183,8 @@ def _full_pins():
         return {k: v for k, v in json.load(f).items() if isinstance(v, dict)}
 
 
-@pytest.mark.parametrize("name", ["cfg2", "cfg3", "cfg5", "cfg4"])
+@pytest.mark.parametrize("name", ["cfg2", "cfg3", "cfg5", "cfg4"] + sorted(n for n in workloads.WORKLOADS
+                                                                            if n.startswith("cfg5_g")))
 def test_full_workload_matches_reference(name, tmp_path):
     """The complete BASELINE workload, formatted here and searched by the HIP
     path, against the reference CPU program's full output (sha256, lines)."""

@@ -8,6 +8,7 @@ cuda:0, as the driver's 8-GPU run does over RCCL): each rank searches its shard,
 the records go to rank 0 in the one gather, the text is assembled by rank 0, and
 both are checked there."""
 import hashlib
+import json
 import os
 import socket
 import subprocess
@@ -19,6 +20,7 @@ import pytest
 
 import cases
 from ghostm_amd.aligner import HIT_DTYPE, Session
+from ghostm_amd.shard import balanced_cuts
 
 pytestmark = pytest.mark.gpu
 
@@ -66,6 +68,109 @@ def test_more_shards_than_queries(dataset, golden):
     assert sum(1 for t in texts if not t) >= 3
 
 
+# batch-cut variants (-l in candidates via the test hook): the unsharded run cuts
+# the chunk into several batches; every shard must replay those cuts (carried
+# lists re-sorted per batch, batches splitting name groups, the dropped carried
+# last query, the stop at an empty first batch: reference aligner.cpp:131-171,
+# 511-514, 687-769). The oracle honours the same hook.
+SHARD_BATCH = [
+    ("syn_dna", "cut13", ["-y", "2"], {"GHOSTM_MAX_LIST_OVERRIDE": "13"}),
+    ("syn_dna", "cut57_b3", ["-b", "3"], {"GHOSTM_MAX_LIST_OVERRIDE": "57"}),
+    ("syn_dna", "cut100", [], {"GHOSTM_MAX_LIST_OVERRIDE": "100"}),
+    ("syn_small", "cut300_b20", ["-b", "20", "-y", "2"], {"GHOSTM_MAX_LIST_OVERRIDE": "300"}),
+    ("syn_small", "cut50", [], {"GHOSTM_MAX_LIST_OVERRIDE": "50"}),
+    ("syn_small", "cut1", [], {"GHOSTM_MAX_LIST_OVERRIDE": "1"}),
+    ("syn_repeat", "cut600_b20", ["-b", "20"], {"GHOSTM_MAX_LIST_OVERRIDE": "600"}),
+    ("syn_chunks", "cut4000_b20", ["-b", "20", "-y", "2"], {"GHOSTM_MAX_LIST_OVERRIDE": "4000"}),
+]
+
+
+class _Env:
+    def __init__(self, env):
+        self.env = env
+
+    def __enter__(self):
+        self.old = {k: os.environ.get(k) for k in self.env}
+        os.environ.update(self.env)
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+_ORACLE_OUT = {}
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("ds,var,opts,env", SHARD_BATCH, ids=[f"{v[0]}/{v[1]}" for v in SHARD_BATCH])
+def test_shards_replay_unsharded_batches(world, ds, var, opts, env, dataset, tmp_path):
+    """Shards of a query set whose chunks need several batches: their rank-order
+    concatenation equals the oracle's unsharded output, and their records the
+    unsharded GPU records."""
+    d = dataset(ds)
+    key = (ds, var)
+    if key not in _ORACLE_OUT:  # one oracle run per variant (syn_chunks takes a minute)
+        _ORACLE_OUT[key] = cases.run_aln(cases.ORACLE, d, opts, env, str(tmp_path / "o.out"))
+    want = _ORACLE_OUT[key]
+    with _Env(env):
+        with Session(_argv(d, opts)) as s:
+            s.run()
+            assert s.output() == want
+            full_hits = s.hits()
+            if var != "cut1":
+                assert s.stats()["batches"] > 1
+        texts, hits = [], []
+        for r in range(world):
+            with Session(_argv(d, opts), shard=(r, world)) as s:
+                s.run()
+                texts.append(s.output())
+                hits.append(s.hits())
+    assert b"".join(texts) == want
+    assert np.concatenate(hits).tobytes() == full_hits.tobytes()
+
+
+def _query_table(d):
+    """Per query of chunk 0: residues (the shard weight) and names."""
+    inf = np.fromfile(f"{d}/q_0.inf", dtype="<u4")
+    nq, L = int(inf[0]), int(inf[1])
+    seq = np.fromfile(f"{d}/q_0.seq", dtype=np.uint8)[: nq * L].reshape(nq, L)
+    notx = seq != 23
+    last = np.where(notx.any(axis=1), L - 1 - np.argmax(notx[:, ::-1], axis=1), 0)
+    names = open(f"{d}/q_0.nam").read().split("\n")[:nq]
+    return (last + 1).tolist(), names
+
+
+def test_shard_starting_at_an_overflow_query(dataset, tmp_path):
+    """A shard whose first query alone exceeds -l in the middle of the unsharded
+    run: batching the shard on its own would end its chunk at once (the
+    reference stops at an empty first batch); replaying the unsharded cuts keeps
+    it. The world is picked so that such a cut exists."""
+    d = dataset("syn_small")
+    prefix = str(tmp_path / "dump")
+    cases.run_aln(cases.ORACLE, d, [], {"GHOSTM_ORACLE_DUMP": prefix}, str(tmp_path / "all.out"))
+    cand = np.fromfile(prefix + ".cand", dtype="<u4").reshape(-1, 4)
+    weights, names = _query_table(d)
+    counts = np.bincount(cand[:, 0], minlength=len(names))
+    # a -l (in candidates) that the chunk's first query fits, and a world with a
+    # cut at a query above it
+    limit, world = next((lim, w) for lim in range(int(counts[0]), int(counts.max()))
+                        for w in range(2, 65)
+                        if any(counts[c] > lim for c in balanced_cuts(weights, names, w)[1:-1] if c < len(names)))
+    env = {"GHOSTM_MAX_LIST_OVERRIDE": str(limit)}
+    want = cases.run_aln(cases.ORACLE, d, [], env, str(tmp_path / "o.out"))
+    assert want  # the unsharded run does not stop at its first query
+    texts = []
+    with _Env(env):
+        for r in range(world):
+            with Session(_argv(d, []), shard=(r, world)) as s:
+                s.run()
+                texts.append(s.output())
+    assert b"".join(texts) == want
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -73,46 +178,92 @@ def _free_port():
 
 
 RANK = textwrap.dedent("""
-    import hashlib, os, sys
+    import json, os, sys
     import numpy as np
     import torch
     import torch.distributed as dist
     sys.path.insert(0, {repo!r})
     from ghostm_amd.aligner import HIT_DTYPE, Session
-    from ghostm_amd.shard import gather_device_records, gather_bytes
+    from ghostm_amd.shard import gather_device_records, gather_bytes, torch_allgather
     rank, world, d, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
+    opts, local = json.loads(sys.argv[5]), sys.argv[6] == "local"
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    with Session(["-i", d + "/q", "-d", d + "/db", "-o", d + "/x", "-D", "0"], shard=(rank, world)) as s:
+    # local: the rank reads and counts only its own queries; the ranks agree on
+    # the unsharded batch plan through the all-gather
+    ex = torch_allgather(dist) if local else None
+    with Session(["-i", d + "/q", "-d", d + "/db", "-o", d + "/x", "-D", "0"] + opts, shard=(rank, world),
+                 exchange=ex) as s:
         s.run()
         recs = s.device_hits()            # on cuda:0
         text = s.output()
+        lo, hi = s.shard_range()
     # the one data-path collective: hit records to rank 0 (gloo here: CPU tensors)
     parts = gather_device_records(recs.cpu(), dist, HIT_DTYPE.itemsize)
     texts = gather_bytes(text, dist)
+    ranges = [None] * world
+    dist.all_gather_object(ranges, (lo, hi))
     if rank == 0:
         with open(out + ".txt", "wb") as f:
             f.write(b"".join(texts))
         np.concatenate([p.numpy() for p in parts]).tofile(out + ".rec")
+        json.dump(ranges, open(out + ".ranges", "w"))
     dist.barrier()
     dist.destroy_process_group()
 """)
 
 
-@pytest.mark.parametrize("ds,var", [("syn_dna", "default"), ("syn_small", "default")])
-def test_two_ranks_gather_to_rank0(ds, var, dataset, golden, tmp_path):
-    d = dataset(ds)
+def _run_ranks(tmp_path, d, world, opts, env, local):
     script = tmp_path / "rank.py"
     script.write_text(RANK.format(repo=cases.REPO))
     out = str(tmp_path / "gathered")
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
-    procs = [subprocess.Popen([sys.executable, str(script), str(r), "2", d, out], env=env,
-                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(2)]
+    e = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), **env)
+    procs = [subprocess.Popen([sys.executable, str(script), str(r), str(world), d, out, json.dumps(opts),
+                               "local" if local else "self"], env=e,
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(world)]
     logs = [p.communicate(timeout=300)[0].decode() for p in procs]
     assert all(p.returncode == 0 for p in procs), "\n".join(logs)
-    text = open(out + ".txt", "rb").read()
+    recs = np.fromfile(out + ".rec", dtype=np.uint8).view(HIT_DTYPE)
+    return open(out + ".txt", "rb").read(), recs, json.load(open(out + ".ranges"))
+
+
+@pytest.mark.parametrize("local", [False, True], ids=["self", "local"])
+@pytest.mark.parametrize("ds,var", [("syn_dna", "default"), ("syn_small", "default")])
+def test_two_ranks_gather_to_rank0(ds, var, local, dataset, golden, tmp_path):
+    d = dataset(ds)
+    text, got, _ = _run_ranks(tmp_path, d, 2, [], {}, local)
     assert _sha(text) == golden["aln"][f"{ds}/{var}"]["sha256"]
     with Session(_argv(d, [])) as s:
         s.run()
         want = s.hits()
-    got = np.fromfile(out + ".rec", dtype=np.uint8).view(HIT_DTYPE)
     assert got.tobytes() == want.tobytes()
+
+
+@pytest.mark.parametrize("ds,var,opts,env,world", [
+    ("syn_dna", "cut13", ["-y", "2"], {"GHOSTM_MAX_LIST_OVERRIDE": "13"}, 3),
+    ("syn_small", "cut300_b20", ["-b", "20", "-y", "2"], {"GHOSTM_MAX_LIST_OVERRIDE": "300"}, 2),
+    ("syn_small", "cut50", [], {"GHOSTM_MAX_LIST_OVERRIDE": "50"}, 8),
+    ("syn_chunks", "cut4000_b20", ["-b", "20", "-y", "2"], {"GHOSTM_MAX_LIST_OVERRIDE": "4000"}, 3),
+    ("syn_chunks", "default", [], {}, 8),
+    ("protein_testset", "y0", [], {}, 10),  # more ranks than queries: empty ranks still exchange
+], ids=lambda v: v if isinstance(v, str) else None)
+def test_rank_local_shards_agree_on_the_batch_plan(ds, var, opts, env, world, dataset, golden, tmp_path):
+    """Rank-local shard sessions (GhostmSessionCreateShardEx over gloo, every rank
+    on cuda:0): each rank reads and counts only its queries, the all-gathered
+    counts give the unsharded batch cuts, and the gathered text and records are
+    the unsharded ones."""
+    d = dataset(ds)
+    if f"{ds}/{var}" in golden["aln"]:
+        want_sha = golden["aln"][f"{ds}/{var}"]["sha256"]
+    else:
+        key = (ds, var)
+        if key not in _ORACLE_OUT:
+            _ORACLE_OUT[key] = cases.run_aln(cases.ORACLE, d, opts, env, str(tmp_path / "o.out"))
+        want_sha = _sha(_ORACLE_OUT[key])
+    text, got, ranges = _run_ranks(tmp_path, d, world, opts, env, True)
+    assert _sha(text) == want_sha
+    with _Env(env):
+        with Session(_argv(d, opts)) as s:
+            s.run()
+            want = s.hits()
+    assert got.tobytes() == want.tobytes()
+    assert ranges[0][0] == 0 and all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))

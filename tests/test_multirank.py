@@ -98,6 +98,39 @@ def test_gather_hits_over_gloo(tmp_path):
         assert got["seq_id"].tolist() == [0.0] * 3 + ([0.5] * 5 if world == 3 else [])
 
 
+AG_WORKER = textwrap.dedent("""
+    import sys
+    import torch.distributed as dist
+    sys.path.insert(0, {repo!r})
+    from ghostm_amd.shard import torch_allgather
+    rank, world = int(sys.argv[1]), int(sys.argv[2])
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ag = torch_allgather(dist)
+    sizes = [(3 * r) % 5 for r in range(world)]  # rank 0 and others send nothing
+    mine = bytes((rank * 16 + k) % 256 for k in range(sizes[rank]))
+    got = ag(mine, sizes)
+    want = b"".join(bytes((r * 16 + k) % 256 for k in range(sizes[r])) for r in range(world))
+    assert got == want, (got, want)
+    assert ag(b"", [0] * world) == b""
+    dist.barrier()
+    dist.destroy_process_group()
+""")
+
+
+def test_torch_allgather_over_gloo(tmp_path):
+    """The all-gather rank-local shard sessions agree on their batch plan with
+    (GhostmAllGatherFn through Session(exchange=...)): ragged per-rank sizes,
+    empty ranks, rank order."""
+    for world in (2, 3):
+        script = tmp_path / "ag.py"
+        script.write_text(AG_WORKER.format(repo=cases.REPO))
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+        procs = [subprocess.Popen([sys.executable, str(script), str(r), str(world)], env=env,
+                                  stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(world)]
+        logs = [p.communicate(timeout=180)[0].decode() for p in procs]
+        assert all(p.returncode == 0 for p in procs), "\n".join(logs)
+
+
 def _read_fasta(path):
     recs, name, seq = [], None, []
     with open(path) as f:
