@@ -389,6 +389,10 @@ def main() -> None:
     if not args.no_e2e:
         runs, files_ok = [], []
         for _ in range(3):
+            # a fresh output path per run (truncating the last run's 0.5 GB file
+            # would free its page-cache pages inside the timed region)
+            if rank == 0 and os.path.exists(out_path):
+                os.remove(out_path)
             if dist is not None:
                 dist.barrier()
             te = time.perf_counter()

@@ -372,7 +372,7 @@ void Session::ApplyShard(uint32_t rank, uint32_t world) {
       }
       c.nseq = whole;
       dev.Free(full);
-      c.seq = std::vector<uint8_t>(c.seq.begin() + (size_t)i0 * c.L, c.seq.begin() + (size_t)(i0 + n) * c.L);
+      c.seq.Own(std::vector<uint8_t>(c.seq.begin() + (size_t)i0 * c.L, c.seq.begin() + (size_t)(i0 + n) * c.L));
       c.names = std::vector<std::string>(c.names.begin() + i0, c.names.begin() + i0 + n);
       c.nseq = n;
       q.global_base += i0;
@@ -561,6 +561,10 @@ Session::Session(const AlignerOptions &opt, uint32_t shard_rank, uint32_t shard_
     const DbChunk &c = d.chunk;
     d.dev = dev.UploadDb(c.seq.data(), c.len, c.keys_count.data(), c.kcl, c.positions.data(), c.npos);
     if (c.nseq) dev.SetDbSubjects(d.dev, c.starts.data(), c.nseq);
+    // resident on the device from here; the host keeps names and starts
+    d.chunk.seq.Release();
+    d.chunk.keys_count.Release();
+    d.chunk.positions.Release();
   }
   {
     std::vector<uint32_t> bases;
@@ -628,6 +632,7 @@ Session::Session(const AlignerOptions &opt, uint32_t shard_rank, uint32_t shard_
     const uint32_t n = q.chunk.nseq, L = q.chunk.L;
     q.dev = dev.UploadQuery(q.chunk.seq.data(), n, L);
     dev.SetQueryGroups(q.dev, q.group_first.data(), q.group_last.data(), (uint32_t)q.group_first.size());
+    q.chunk.seq.Release();  // resident on the device (qlen and names stay on the host)
   }
   if (local) PlanExchange(shard_rank, shard_world, *ex, chunk_nseq, rank_lo);
   dev.Synchronize();

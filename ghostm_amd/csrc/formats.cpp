@@ -16,6 +16,52 @@
 
 namespace ghostm {
 
+template <class T>
+bool FileArray<T>::Map(const std::string &path, uint64_t off, size_t n) {
+  *this = FileArray();
+  if (n == 0) return true;
+  const size_t bytes = n * sizeof(T);
+  const int fd = open(path.c_str(), O_RDONLY);
+  struct stat st {};
+  const bool ok = fd >= 0 && fstat(fd, &st) == 0;
+  if (ok && (uint64_t)st.st_size >= off + bytes) {
+    void *m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+    if (m != MAP_FAILED) {
+      const size_t len = (size_t)st.st_size;
+      hold_ = std::shared_ptr<const void>(m, [len](const void *q) { munmap(const_cast<void *>(q), len); });
+      p_ = reinterpret_cast<const T *>(static_cast<const char *>(m) + off);
+      n_ = n;
+      close(fd);
+      return true;
+    }
+  }
+  // short or unmappable: what the file holds, zeros after it
+  std::vector<T> v(n, T());
+  if (ok) {
+    char *dst = reinterpret_cast<char *>(v.data());
+    size_t done = 0;
+    while (done < bytes) {
+      const ssize_t r = pread(fd, dst + done, bytes - done, (off_t)(off + done));
+      if (r <= 0) break;
+      done += (size_t)r;
+    }
+  }
+  if (fd >= 0) close(fd);
+  Own(std::move(v));
+  return ok;
+}
+
+template <class T>
+void FileArray<T>::Own(std::vector<T> v) {
+  auto own = std::make_shared<std::vector<T>>(std::move(v));
+  p_ = own->data();
+  n_ = own->size();
+  hold_ = own;
+}
+
+template class FileArray<uint8_t>;
+template class FileArray<uint32_t>;
+
 uint8_t ProteinCode(unsigned char ch) {
   struct Table {
     uint8_t t[256];
@@ -124,9 +170,7 @@ bool QueryFile::ReadChunk(uint32_t id, QueryChunk *q) const {
   ReadRaw(f, &q->nseq, 1);
   ReadRaw(f, &q->L, 1);
   q->names = ReadNameLines(base + ".nam", q->nseq, nullptr);
-  q->seq.assign((size_t)q->nseq * q->L, 0);
-  std::ifstream s((base + ".seq").c_str(), std::ios::binary);
-  if (s) ReadRaw(s, q->seq.data(), q->seq.size());
+  q->seq.Map(base + ".seq", 0, (size_t)q->nseq * q->L);
   return true;
 }
 
@@ -230,17 +274,8 @@ void QueryChunkIndex::ReadSlice(uint32_t i0, uint32_t n, QueryChunk *q) const {
     if (!names.empty()) q->names[k] = names[i];
     else q->names[k].assign(nam, line[i], line[i + 1] - 1 - line[i]);
   }
-  q->seq.assign((size_t)n * L, 0);
-  const int fd = open((base + ".seq").c_str(), O_RDONLY);
-  if (fd < 0) return;
-  size_t done = 0;
-  const size_t want = q->seq.size();
-  while (done < want) {
-    const ssize_t r = pread(fd, q->seq.data() + done, want - done, (off_t)((size_t)i0 * L + done));
-    if (r <= 0) break;  // a short file leaves zeros, as ReadChunk
-    done += (size_t)r;
-  }
-  close(fd);
+  // (a short file leaves zeros, as ReadChunk)
+  q->seq.Map(base + ".seq", (uint64_t)i0 * L, (size_t)n * L);
 }
 
 DbFile::DbFile(const std::string &p) : prefix(p) {
@@ -266,20 +301,15 @@ bool DbFile::ReadChunk(uint32_t id, DbChunk *d) const {
     std::ifstream s((base + ".pos").c_str(), std::ios::binary);
     if (s) ReadRaw(s, d->starts.data(), d->nseq);
   }
-  d->seq.assign(d->len, 0);
-  {
-    std::ifstream s((base + ".seq").c_str(), std::ios::binary);
-    if (s) ReadRaw(s, d->seq.data(), d->len);
-  }
+  d->seq.Map(base + ".seq", 0, d->len);
   std::ifstream s((base + ".ind").c_str(), std::ios::binary);
   if (s) {
     ReadRaw(s, &d->seed, 1);
     ReadRaw(s, &d->kcl, 1);
     ReadRaw(s, &d->npos, 1);
-    d->keys_count.assign(d->kcl, 0);
-    d->positions.assign(d->npos, 0);
-    ReadRaw(s, d->keys_count.data(), d->kcl);
-    ReadRaw(s, d->positions.data(), d->npos);
+    s.close();
+    d->keys_count.Map(base + ".ind", 12, d->kcl);
+    d->positions.Map(base + ".ind", 12 + 4 * (uint64_t)d->kcl, d->npos);
   }
   return true;
 }

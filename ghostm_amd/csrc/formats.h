@@ -10,17 +10,43 @@
 // DBReader/DB/Index (db_reader.cpp:34-77, db.cpp:36-123, index.h:86-126).
 #pragma once
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
 namespace ghostm {
+
+// A read-only array of a chunk file's contents: a private, pre-faulted mapping
+// of the file (its page-cache pages: no copy, no zero-fill page faults), or
+// an owned buffer (a slice, or a file shorter than its header says, the rest
+// zeros as the reference's unchecked reads leave it).
+template <class T>
+class FileArray {
+ public:
+  const T *data() const { return p_; }
+  size_t size() const { return n_; }
+  bool empty() const { return n_ == 0; }
+  const T &operator[](size_t i) const { return p_[i]; }
+  const T *begin() const { return p_; }
+  const T *end() const { return p_ + n_; }
+  // n elements of `path` from byte offset `off`; false if it cannot be opened
+  // (the array is then n zeros)
+  bool Map(const std::string &path, uint64_t off, size_t n);
+  void Own(std::vector<T> v);
+  void Release() { *this = FileArray(); }
+
+ private:
+  const T *p_ = nullptr;
+  size_t n_ = 0;
+  std::shared_ptr<const void> hold_;  // the mapping or the owned vector
+};
 
 struct QueryChunk {
   uint32_t id = 0;
   uint32_t nseq = 0;
   uint32_t L = 0;                  // fixed record width (X padded)
   std::vector<std::string> names;  // one per record
-  std::vector<uint8_t> seq;        // nseq * L codes
+  FileArray<uint8_t> seq;          // nseq * L codes
 };
 
 // WriteOutput's query length (reference aligner.cpp:959-961): the index of the
@@ -60,10 +86,10 @@ struct DbChunk {
   uint32_t len = 0;                // concatenated length incl. END separators
   std::vector<std::string> names;
   std::vector<uint32_t> starts;    // subject start offsets (.pos)
-  std::vector<uint8_t> seq;
+  FileArray<uint8_t> seq;
   uint32_t seed = 0, kcl = 0, npos = 0;
-  std::vector<uint32_t> keys_count;
-  std::vector<uint32_t> positions;
+  FileArray<uint32_t> keys_count;
+  FileArray<uint32_t> positions;
   // Subject containing concatenated position p (DB::GetID, db.h:106-135).
   uint32_t SubjectOf(uint32_t p) const;
 };

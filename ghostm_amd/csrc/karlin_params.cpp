@@ -17,6 +17,13 @@
 //   Lambda             karlin.cpp:187-289 (Newton-Raphson, bisection fallback)
 //   Entropy            karlin.cpp:297-324 (H from lambda)
 //   KParameter         karlin.cpp:68-180 (K from lambda and H)
+//
+// The routines restated here carry this notice in the reference
+// (karlin.cpp:1-4), retained as it asks:
+//   karlin.c
+//   Copyright (c) 2005, Michael Cameron
+//   Permission to use this code is freely granted under the BSD license
+//   agreement, provided that this statement is retained.
 #include <cmath>
 #include <cstdint>
 #include <stdexcept>

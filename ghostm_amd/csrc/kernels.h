@@ -568,7 +568,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed_hash(SeedArgs a) {
       uint32_t prev_pos = prv[u];
       if (lane > 0 && pj == j) prev_pos = pp;
       if (j != 0xFFFFFFFFu) {
-        const uint32_t d0 = j * a.shift;
+        const uint32_t d0 = __umul24(j, a.shift);  // j < 128: full-rate 24-bit multiply
         const uint32_t bin = (pos[u] - d0) >> a.log_region;
         const bool dup = prev_pos != 0xFFFFFFFFu && ((prev_pos - d0) >> a.log_region) == bin;
         if (!dup) table.Insert(bin);
@@ -607,7 +607,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   constexpr uint32_t kChunks = KE * kW;
   constexpr uint32_t kNone = 0xFFFFFFFFu;
   static_assert((FSLOTS & (FSLOTS - 1)) == 0 && TSLOTS * 2 >= QCAP * 3 && TSLOTS % BLOCK == 0, "filter shape");
-  __shared__ uint32_t s_beg[kMaxLists];
+  __shared__ uint32_t s_delta[kMaxLists];     // list j: position index of entry i = i + s_delta[j]
   __shared__ uint32_t s_off[kMaxLists + 1];
   __shared__ uint8_t s_cfirst[kChunks];
   __shared__ __attribute__((aligned(16))) uint32_t s_emit[kMaxSlotCap];
@@ -620,14 +620,15 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   const uint32_t nl = a.nlists;
   for (uint32_t k = tid; k < kFWords + TSLOTS; k += BLOCK) s_dyn[k] = 0;
   if (tid == 0) s_qn = 0;
-  uint32_t len = 0;
+  uint32_t len = 0, beg = 0;
   if (tid < nl) {
-    s_beg[tid] = a.list_beg[(size_t)q * nl + tid];
+    beg = a.list_beg[(size_t)q * nl + tid];
     len = a.list_len[(size_t)q * nl + tid];
   }
   const uint32_t excl = BlockExclusiveScan(len, s_part, &s_total);
   if (tid < nl) {
     s_off[tid] = excl;
+    s_delta[tid] = beg - excl;
     for (uint32_t c = (excl + 63) >> 6; (c << 6) < excl + len && c < kChunks; ++c) s_cfirst[c] = (uint8_t)tid;
   }
   if (tid == 0) s_off[nl] = s_total;
@@ -649,10 +650,10 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
       if (i < n) {
         uint32_t j = s_cfirst[c];
         while (s_off[j + 1] <= i) ++j;
-        const uint32_t r = i - s_off[j];
-        pos[u] = a.positions[s_beg[j] + r];
+        const uint32_t at = i + s_delta[j];  // = list_beg[j] + (i - s_off[j])
+        pos[u] = a.positions[at];
         lst[u] = j;
-        if (lane == 0 && r > 0) prv[u] = a.positions[s_beg[j] + r - 1];
+        if (lane == 0 && i != s_off[j]) prv[u] = a.positions[at - 1];
       }
     }
 #pragma unroll
@@ -663,7 +664,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
       if (lane > 0 && pj == j) prev_pos = pp;
       uint32_t x = kNone;
       if (j != kNone) {
-        const uint32_t d0 = j * a.shift;
+        const uint32_t d0 = __umul24(j, a.shift);  // j < 128: full-rate 24-bit multiply
         const uint32_t b = (pos[u] - d0) >> a.log_region;
         const bool dup = prev_pos != kNone && ((prev_pos - d0) >> a.log_region) == b;
         if (!dup) {
