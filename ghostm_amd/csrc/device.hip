@@ -1160,7 +1160,7 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
     sa.ncols = I.tb_ncols.as<uint32_t>();
     sa.hist = hist2;
     sa.cells = a.cells ? a.cells + 1 : nullptr;
-    // every CU one 1024-thread workgroup, looping over the sorted pairs
+    // every CU one workgroup (kScanBlock threads), looping over the sorted pairs
     const uint32_t pairs_per_block = (kern::kScanBlock / 64) * lay.gpw;
     const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)I.cus,
                                                                      (n + pairs_per_block - 1) / pairs_per_block));

@@ -2290,7 +2290,10 @@ __global__ void k_records(const uint32_t *sel_count, const SlotHit *slots, const
 // k_tb_scan and the hits by j* + 1 for the key kernel, so each wave's lane
 // groups run windows of about the same length.
 constexpr uint32_t kSortBins = 1024;   // counting-sort keys (column counts), clamped
-constexpr int kScanBlock = 1024;       // one workgroup per CU: the pair table fills the LDS
+// one workgroup per CU (the pair table fills the LDS) of 12 waves: 3 per SIMD
+// leave 168 VGPRs, room for an 8-row read-ahead (1024 threads, 128 VGPRs and a
+// 4-row read-ahead measured 56.5 against 55.8 ms of K3 per step, same box)
+constexpr int kScanBlock = 768;
 constexpr uint32_t kPairCodes = 26;    // DB codes 0..25 (25 = END) index the pair table
 // dwords per (a, b) code pair: query codes 0..31 plus one, an odd stride, so the
 // bank of entry (a, b, q), (pair * 33 + q) mod 32, spreads lanes reading the same
@@ -2648,12 +2651,11 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
       auto T = [&](int u) { return *reinterpret_cast<const uint32_t *>(tp + ((qoff[u >> 2] >> (8 * (u & 3))) & 0xFFu)); };
       uint32_t diag = diag0, F = fin, cm = sig;
       if constexpr (FRAMED) {
-        // software-pipelined by chunks of four rows: the next chunk's four table
-        // reads are issued before this chunk's rows, and each row's diagonal
-        // sum is formed one row ahead, from the old H just before the row above
-        // overwrites it (t + tn + two sums: fewer live registers than eight
-        // reads and eight sums)
-        constexpr int CH = 4;
+        // software-pipelined by chunks of eight rows: the next chunk's eight
+        // table reads are issued before this chunk's rows, and each row's
+        // diagonal sum is formed one row ahead, from the old H just before the
+        // row above overwrites it
+        constexpr int CH = 8;
         uint32_t t[CH], tn[CH];
 #pragma unroll
         for (int u = 0; u < CH; ++u) t[u] = T(u);
@@ -2681,7 +2683,11 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
             F = SWAR ? W(G) + NEXT32 : W(G + NEXT);
             sc = sn;
           }
-          cm = C::Max3(C::Max3(H[k], H[k + 1], H[k + 2]), H[k + 3], cm);
+          if constexpr (CH == 8)
+            cm = C::Max3(C::Max3(H[k], H[k + 1], H[k + 2]), C::Max3(H[k + 3], H[k + 4], H[k + 5]),
+                         C::Max3(H[k + 6], H[k + 7], cm));
+          else
+            cm = C::Max3(C::Max3(H[k], H[k + 1], H[k + 2]), H[k + 3], cm);
           if (k + CH < S) {
 #pragma unroll
             for (int u = 0; u < CH; ++u) t[u] = tn[u];
