@@ -109,6 +109,7 @@ struct DevDb {
   uint32_t len = 0, kcl = 0, npos = 0;
   const uint8_t *Residues() const { return seq.as<uint8_t>() + kDbFront; }
   DevBuf subj;                     // subject starts (device merge)
+  DevBuf subj_bucket;              // kern::SubjectOfBucketed's table
   uint32_t nsubj = 0;
 };
 
@@ -385,6 +386,7 @@ void DeviceModule::Free(DevDb *d) {
   d->kc.Release();
   d->pos.Release();
   d->subj.Release();
+  d->subj_bucket.Release();
   delete d;
 }
 
@@ -405,6 +407,20 @@ void DeviceModule::SetDbSubjects(DevDb *d, const uint32_t *starts, uint32_t nsub
   d->nsubj = nsubj;
   d->subj.Reserve((size_t)nsubj * 4);
   if (nsubj) HIP_CHECK(hipMemcpy(d->subj.p, starts, (size_t)nsubj * 4, hipMemcpyHostToDevice));
+  // bucket[k] = the last subject starting at or before k << shift (kNoSlot: none),
+  // for k = 0 .. (len >> shift) + 1
+  if (nsubj) {
+    const uint32_t nb = (d->len >> kern::kSubjBucketShift) + 2;
+    std::vector<uint32_t> bucket(nb);
+    uint32_t s = 0;
+    for (uint32_t k = 0; k < nb; ++k) {
+      const uint64_t at = (uint64_t)k << kern::kSubjBucketShift;
+      while (s + 1 < nsubj && starts[s + 1] <= at) ++s;
+      bucket[k] = starts[s] <= at ? s : kern::kNoSlot;
+    }
+    d->subj_bucket.Reserve((size_t)nb * 4);
+    HIP_CHECK(hipMemcpy(d->subj_bucket.p, bucket.data(), (size_t)nb * 4, hipMemcpyHostToDevice));
+  }
 }
 
 void DeviceModule::Synchronize() {
@@ -1117,7 +1133,8 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
     const dim3 g256((n + 255) / 256), b256(256);
     const uint32_t *subj = d && d->nsubj ? d->subj.as<uint32_t>() : nullptr;
     hipLaunchKernelGGL(kern::k_tb_prep, g256, b256, 0, S(stream_), a.qid, a.end, n, a.base, subj,
-                       subj ? d->nsubj : 0u, d ? d->len : 0u, I.tb_width.as<uint32_t>(),
+                       subj ? d->nsubj : 0u, subj ? d->subj_bucket.as<uint32_t>() : nullptr, d ? d->len : 0u,
+                       I.tb_width.as<uint32_t>(),
                        I.tb_ncols.as<uint32_t>(), hist2);  // empty slots -> hist2[0]
     const uint32_t ps = std::max<uint32_t>(pair_span, 1);
     const uint32_t runs_per_span = (ps + kern::kPairRun - 1) / kern::kPairRun;
@@ -1294,7 +1311,10 @@ void DeviceModule::MergeLaunch(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, 
   m.end = I.end_out.as<uint32_t>();
   m.cand_qid = I.cand_qid.as<uint32_t>();
   m.subj_start = d->subj.as<uint32_t>();
+  m.subj_bucket = d->subj_bucket.as<uint32_t>();
   m.nsubj = d->nsubj;
+  m.sid_bits = 0;
+  while (m.sid_bits < 32 && (d->nsubj - 1) >> m.sid_bits) ++m.sid_bits;
   m.dblen = d->len;
   m.keys = I.keys.as<unsigned long long>();
   m.best = best;

@@ -1908,6 +1908,7 @@ struct MergeArgs {
   const uint32_t *end;                 // batch-relative, absolute DB position
   const uint32_t *cand_qid;            // absolute
   const uint32_t *subj_start;          // DB chunk subject starts (.pos)
+  const uint32_t *subj_bucket;         // SubjectOfBucketed's table (null: binary search)
   uint32_t nsubj, dblen;
   unsigned long long *keys;            // scratch, batch-relative
   uint32_t best, cap;                  // -b and slots per group (max(best, 1))
@@ -1918,6 +1919,7 @@ struct MergeArgs {
   uint32_t *tb_end;                    // [ng*cap]
   uint32_t wave_cap;                   // k_merge_wave: largest group kept in LDS (<= kMergeCap)
   uint32_t wave_small;                 // k_merge_wave: the small launch's largest group
+  uint32_t sid_bits;                   // bits of a subject index (nsubj - 1 < 2^sid_bits)
   // the batch's candidate range (absolute): a group's candidates are its
   // queries' candidates clipped to it (a batch may cut a name group)
   unsigned long long cand_lo, cand_hi;
@@ -1950,6 +1952,28 @@ __device__ inline uint32_t SubjectOf(const uint32_t *starts, uint32_t n, uint32_
     if (starts[mid] < p) lo = mid + 1; else hi = mid - 1;
   }
   return 0xFFFFFFFFu;
+}
+
+// DB::GetID through a bucket table: bucket[k] = the last subject starting at or
+// before position k << kSubjBucketShift (kNoSlot: none). A position's subject
+// is the last one starting at or before it, which is what the reference's
+// search returns for every position inside the DB; it lies between the
+// position's bucket entry and the next one (about one subject per bucket), so
+// this takes two or three dependent loads instead of a 15-step binary search.
+// Positions outside the table take the reference's search.
+constexpr uint32_t kSubjBucketShift = 8;
+__device__ inline uint32_t SubjectOfBucketed(const uint32_t *starts, uint32_t n, uint32_t len, const uint32_t *bucket,
+                                             uint32_t p) {
+  if (bucket && p < len) {
+    const uint32_t k = p >> kSubjBucketShift;
+    uint32_t s = bucket[k];
+    const uint32_t s1 = bucket[k + 1];
+    if (s != 0xFFFFFFFFu) {
+      while (s < s1 && starts[s + 1] <= p) ++s;
+      return s;
+    }
+  }
+  return SubjectOf(starts, n, len, p);
 }
 
 struct ScoreDescending {
@@ -1990,7 +2014,7 @@ __device__ inline void MergeGroup(const MergeArgs &a, uint32_t g) {
       ++count;
     } else {
       const unsigned long long c = b + idx;
-      const uint32_t sid = SubjectOf(a.subj_start, a.nsubj, a.dblen, a.end[c]);
+      const uint32_t sid = SubjectOfBucketed(a.subj_start, a.nsubj, a.dblen, a.subj_bucket, a.end[c]);
       bool seen = false;
       for (uint32_t k = 0; k < count; ++k) seen |= sid_out[k] == sid;
       if (!seen) {
@@ -2171,13 +2195,22 @@ __device__ inline void MergeWaveGroup(const MergeArgs &a, uint32_t g, uint32_t l
       carried = idx >= nnew;
       if (!carried) {
         c = (uint32_t)(b + idx);
-        sid = SubjectOf(a.subj_start, a.nsubj, a.dblen, a.end[c]);
+        sid = SubjectOfBucketed(a.subj_start, a.nsubj, a.dblen, a.subj_bucket, a.end[c]);
         for (uint32_t k = 0; k < count; ++k) ok = ok && taken[k] != sid;
       }
     }
-    for (uint32_t t = 0; t + 1 < m; ++t) {
-      const uint32_t st = (uint32_t)__shfl((int)sid, (int)t);
-      if (!carried && lane > t && st == sid) ok = false;
+    // first occurrence by lane order: the lanes holding the same subject, from
+    // one ballot per subject-index bit (sid < nsubj; carried lanes and lanes
+    // past m hold kNoSlot and take no part)
+    {
+      const bool real = lane < m && !carried;
+      unsigned long long peers = __ballot(real);
+      for (uint32_t bit = 0; bit < a.sid_bits; ++bit) {
+        const bool one = (sid >> bit) & 1u;
+        const unsigned long long bal = __ballot(one);
+        peers &= one ? bal : ~bal;
+      }
+      if (real && (peers & ((1ull << lane) - 1))) ok = false;
     }
     const unsigned long long bal = __ballot(ok);
     const uint32_t rank = __popcll(bal & ((1ull << lane) - 1));
@@ -2306,8 +2339,8 @@ constexpr uint32_t kPairWords = kPairCodes * kPairCodes * kPairStride;
 // reset to 0.
 __global__ __launch_bounds__(256) void k_tb_prep(const uint32_t *qid, const uint32_t *end, uint32_t n,
                                                  uint32_t base, const uint32_t *subj, uint32_t nsubj,
-                                                 uint32_t dblen, uint32_t *width, uint32_t *ncols,
-                                                 uint32_t *empty) {
+                                                 const uint32_t *subj_bucket, uint32_t dblen, uint32_t *width,
+                                                 uint32_t *ncols, uint32_t *empty) {
   __shared__ uint32_t s_empty;
   if (threadIdx.x == 0) s_empty = 0;
   __syncthreads();
@@ -2318,7 +2351,7 @@ __global__ __launch_bounds__(256) void k_tb_prep(const uint32_t *qid, const uint
       const uint32_t p0 = end[k];
       w = p0 < base ? p0 + 1 : base;
       if (nsubj) {
-        const uint32_t sid = SubjectOf(subj, nsubj, dblen, p0);
+        const uint32_t sid = SubjectOfBucketed(subj, nsubj, dblen, subj_bucket, p0);
         if (sid != 0xFFFFFFFFu) w = min(w, p0 - subj[sid] + 1);
       }
     }
