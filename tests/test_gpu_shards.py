@@ -245,6 +245,7 @@ def test_two_ranks_gather_to_rank0(ds, var, local, dataset, golden, tmp_path):
     ("syn_chunks", "cut4000_b20", ["-b", "20", "-y", "2"], {"GHOSTM_MAX_LIST_OVERRIDE": "4000"}, 3),
     ("syn_chunks", "default", [], {}, 8),
     ("protein_testset", "y0", [], {}, 10),  # more ranks than queries: empty ranks still exchange
+    ("syn_chunks", "S1", ["-S", "1"], {}, 3),  # -S: the selected chunks only, global indices from there
 ], ids=lambda v: v if isinstance(v, str) else None)
 def test_rank_local_shards_agree_on_the_batch_plan(ds, var, opts, env, world, dataset, golden, tmp_path):
     """Rank-local shard sessions (GhostmSessionCreateShardEx over gloo, every rank
@@ -267,3 +268,25 @@ def test_rank_local_shards_agree_on_the_batch_plan(ds, var, opts, env, world, da
             want = s.hits()
     assert got.tobytes() == want.tobytes()
     assert ranges[0][0] == 0 and all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
+
+
+def test_rank_local_names_file_shorter_than_the_chunk(dataset, tmp_path):
+    """A .nam with fewer lines than the chunk's queries: the reference reads the
+    missing names as empty (query_reader.cpp, ReadNameLines' getline path), and a
+    rank-local shard reads its names the same way (QueryChunkIndex falls back to
+    the full name list), so shards still concatenate to the unsharded output."""
+    import shutil
+
+    src = dataset("syn_small")
+    d = tmp_path / "ds"
+    shutil.copytree(src, d)
+    lines = (d / "q_0.nam").read_bytes().split(b"\n")
+    (d / "q_0.nam").write_bytes(b"\n".join(lines[:-6]))  # last names missing, last line unterminated
+    with Session(_argv(str(d), [])) as s:
+        s.run()
+        want = s.output()
+        want_hits = s.hits()
+    assert want
+    text, got, _ = _run_ranks(tmp_path, str(d), 3, [], {}, True)
+    assert text == want
+    assert got.tobytes() == want_hits.tobytes()
