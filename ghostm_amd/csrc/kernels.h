@@ -431,13 +431,9 @@ struct BinTable {
 // (c(b) > 0 or b = 0) and c(b) + c(b+1) >= T per occupied slot, the count to
 // counts[q], and for queries with <= slot_cap candidates the emitted bins in
 // ascending order into the query's slot.
-// FSLOTS > 0: s_flt is k_seed_filter's presence bitmap (two bits per cell,
-// FSLOTS cells, cell = bin mod FSLOTS); a bin whose b + 1 cell was never seen has
-// c(b + 1) = 0 exactly, so its emission test needs no table lookup.
-template <uint32_t BLOCK, uint32_t TSLOTS, uint32_t FSLOTS = 0>
+template <uint32_t BLOCK, uint32_t TSLOTS>
 __device__ __forceinline__ void EmitFromTable(const SeedArgs &a, uint32_t q, uint32_t *s_tab, uint32_t *s_emit,
-                                              uint32_t *s_part, uint32_t *s_total_p,
-                                              const uint32_t *s_flt = nullptr) {
+                                              uint32_t *s_part, uint32_t *s_total_p) {
   constexpr uint32_t kPer = TSLOTS / BLOCK;
   BinTable<TSLOTS> table{s_tab};
   const uint32_t tid = threadIdx.x;
@@ -455,12 +451,7 @@ __device__ __forceinline__ void EmitFromTable(const SeedArgs &a, uint32_t q, uin
       occ &= occ - 1;
       const uint32_t v = s_tab[tid + k * BLOCK];
       const uint32_t c = (v >> 3) & 0xFFu;
-      bool next_seen = true;  // c(bin + 1) may be > 0
-      if constexpr (FSLOTS != 0) {
-        const uint32_t cell = (v >> 11) & (FSLOTS - 1);  // bin + 1 = v >> 11
-        next_seen = (s_flt[cell >> 4] >> ((cell & 15) * 2)) & 1u;
-      }
-      if (c >= thr || (next_seen && c + table.Count(v >> 11) >= thr)) {
+      if (c >= thr || c + table.Count(v >> 11) >= thr) {  // bin + 1 = v >> 11
         mask |= 1u << k;
         ++mine;
       }
@@ -721,7 +712,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   BinTable<TSLOTS> table{s_tab};
   for (uint32_t k = tid; k < qn; k += BLOCK) table.Insert(s_q[k]);
   __syncthreads();
-  EmitFromTable<BLOCK, TSLOTS, FSLOTS>(a, q, s_tab, s_emit, s_part, &s_total, s_flt);
+  EmitFromTable<BLOCK, TSLOTS>(a, q, s_tab, s_emit, s_part, &s_total);
 }
 
 // Slot -> compact copy for queries whose candidates fit their slot.
