@@ -145,7 +145,7 @@ struct DeviceModule::Impl {
   DevBuf tb_width, tb_ncols, tb_key, tb_order1, tb_order2, tb_sort, tb_pair_a, tb_pair_b, tb_best;
   int cus = 256;
   // K4 work
-  DevBuf keys, sel_count, sel_cand, sel_sid, slot_hits, sel_from;
+  DevBuf keys, sel_count, sel_score, sel_sid, slot_hits, sel_from;
   struct MergeState {  // the launched, not yet collected K4/K3
     bool active = false;
     uint32_t ng = 0;
@@ -1293,7 +1293,7 @@ void DeviceModule::MergeLaunch(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, 
   I.keys.Reserve((n + slots) * 8 + 8);  // per group: its candidates and cap carried keys
   I.sel_from.Reserve(slots * 4);
   I.sel_count.Reserve((size_t)ng * 4);
-  I.sel_cand.Reserve(slots * 4);
+  I.sel_score.Reserve(slots * 4);
   I.sel_sid.Reserve(slots * 4);
   I.tb_qid.Reserve(slots * 4);
   I.tb_end.Reserve(slots * 4);
@@ -1320,7 +1320,7 @@ void DeviceModule::MergeLaunch(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, 
   m.best = best;
   m.cap = cap;
   m.sel_count = I.sel_count.as<uint32_t>();
-  m.sel_cand = I.sel_cand.as<uint32_t>();
+  m.sel_score = I.sel_score.as<uint32_t>();
   m.sel_sid = I.sel_sid.as<uint32_t>();
   m.tb_qid = I.tb_qid.as<uint32_t>();
   m.tb_end = I.tb_end.as<uint32_t>();
@@ -1381,8 +1381,8 @@ void DeviceModule::MergeLaunch(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, 
   LaunchTraceback(a, q, (uint32_t)slots, d, cap);
   HIP_CHECK(hipEventRecord(I.ev_t1, S(stream_)));
   hipLaunchKernelGGL(kern::k_finalize, dim3((uint32_t)((slots + 255) / 256)), dim3(256), 0, S(stream_),
-                     I.sel_count.as<uint32_t>(), I.sel_cand.as<uint32_t>(), I.sel_sid.as<uint32_t>(),
-                     I.score_out.as<uint32_t>(), I.end_out.as<uint32_t>(), I.tb_start.as<uint32_t>(),
+                     I.sel_count.as<uint32_t>(), I.sel_score.as<uint32_t>(), I.sel_sid.as<uint32_t>(),
+                     I.tb_end.as<uint32_t>(), I.tb_start.as<uint32_t>(),
                      I.tb_ml.as<uint32_t>(), d->subj.as<uint32_t>(), ng, cap, pass.chunk,
                      m.sel_from, m.carry, I.slot_hits.as<kern::SlotHit>(),
                      I.tb_counters.as<unsigned long long>() + 2);

@@ -1913,7 +1913,7 @@ struct MergeArgs {
   unsigned long long *keys;            // scratch, batch-relative
   uint32_t best, cap;                  // -b and slots per group (max(best, 1))
   uint32_t *sel_count;                 // [ng]
-  uint32_t *sel_cand;                  // [ng*cap] batch-relative candidate
+  uint32_t *sel_score;                 // [ng*cap] the selected candidate's score (k_finalize)
   uint32_t *sel_sid;                   // [ng*cap]
   uint32_t *tb_qid;                    // [ng*cap] K3 request (0xFFFFFFFF = empty)
   uint32_t *tb_end;                    // [ng*cap]
@@ -2001,14 +2001,14 @@ __device__ inline void MergeGroup(const MergeArgs &a, uint32_t g) {
   // the whole group is sorted
   stdsort::LazySort<unsigned long long, ScoreDescending> order(keys, (long)total, ScoreDescending());
   uint32_t *sid_out = a.sel_sid + so;
-  uint32_t *cand_out = a.sel_cand + so;
+  uint32_t *score_out = a.sel_score + so;
   uint32_t count = 0;
   for (unsigned long long i = 0; i < total; ++i) {
     while ((long)i >= order.done) order.Advance();
     const uint32_t idx = (uint32_t)keys[i];
     if (idx >= n) {  // a carried result: kept as it is
       sid_out[count] = kNoSlot;
-      cand_out[count] = kNoSlot;
+      score_out[count] = 0;
       if (a.sel_from) a.sel_from[so + count] = idx - (uint32_t)n;
       a.tb_qid[so + count] = kNoSlot;
       ++count;
@@ -2019,7 +2019,7 @@ __device__ inline void MergeGroup(const MergeArgs &a, uint32_t g) {
       for (uint32_t k = 0; k < count; ++k) seen |= sid_out[k] == sid;
       if (!seen) {
         sid_out[count] = sid;
-        cand_out[count] = (uint32_t)c;
+        score_out[count] = a.score[c];
         if (a.sel_from) a.sel_from[so + count] = kNoSlot;
         a.tb_qid[so + count] = a.cand_qid[a.out_base + c];
         a.tb_end[so + count] = a.end[c];
@@ -2188,10 +2188,12 @@ __device__ inline void MergeWaveGroup(const MergeArgs &a, uint32_t g, uint32_t l
     // result is taken unchanged and claims no subject (sid kNoSlot matches no
     // real subject)
     const uint32_t m = min(64u, done - walked);
-    uint32_t sid = kNoSlot, c = 0, idx = 0;
+    uint32_t sid = kNoSlot, c = 0, idx = 0, sc = 0;
     bool ok = lane < m, carried = false;
     if (ok) {
-      idx = (uint32_t)K[walked + lane];
+      const unsigned long long key = K[walked + lane];
+      idx = (uint32_t)key;
+      sc = (uint32_t)(key >> 32);
       carried = idx >= nnew;
       if (!carried) {
         c = (uint32_t)(b + idx);
@@ -2219,11 +2221,11 @@ __device__ inline void MergeWaveGroup(const MergeArgs &a, uint32_t g, uint32_t l
       const uint32_t at = count + rank;
       a.sel_sid[so + at] = sid;
       if (carried) {
-        a.sel_cand[so + at] = kNoSlot;
+        a.sel_score[so + at] = 0;
         a.sel_from[so + at] = idx - nnew;
         a.tb_qid[so + at] = kNoSlot;
       } else {
-        a.sel_cand[so + at] = c;
+        a.sel_score[so + at] = sc;
         if (a.sel_from) a.sel_from[so + at] = kNoSlot;
         a.tb_qid[so + at] = a.cand_qid[a.out_base + c];
         a.tb_end[so + at] = a.end[c];
@@ -2258,9 +2260,11 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_merge_wave(MergeArgs a) {
 }
 
 // Selected slots -> records: a new hit rebased to its subject after K3, a
-// carried one copied (sel_from), so out[] is the group's new result list.
-__global__ void k_finalize(const uint32_t *sel_count, const uint32_t *sel_cand,
-                           const uint32_t *sel_sid, const uint32_t *score, const uint32_t *end,
+// carried one copied (sel_from), so out[] is the group's new result list. K4
+// left each new hit's score and end in its slot (sel_score, tb_end), so every
+// read here but the subject start is slot-indexed.
+__global__ void k_finalize(const uint32_t *sel_count, const uint32_t *sel_score,
+                           const uint32_t *sel_sid, const uint32_t *sel_end,
                            const uint32_t *tb_start, const uint32_t *tb_ml,
                            const uint32_t *subj_start, uint32_t ng, uint32_t cap, uint32_t chunk,
                            const uint32_t *sel_from, const SlotHit *carry, SlotHit *out,
@@ -2273,8 +2277,8 @@ __global__ void k_finalize(const uint32_t *sel_count, const uint32_t *sel_cand,
       if (sel_from && sel_from[s] != kNoSlot) {
         out[s] = carry[(size_t)g * cap + sel_from[s]];
       } else {
-        const uint32_t c = sel_cand[s], sid = sel_sid[s], pos = subj_start[sid];
-        out[s] = SlotHit{sid, score[c], tb_start[s] - pos, end[c] - pos, tb_ml[s], chunk};
+        const uint32_t sid = sel_sid[s], pos = subj_start[sid];
+        out[s] = SlotHit{sid, sel_score[s], tb_start[s] - pos, sel_end[s] - pos, tb_ml[s], chunk};
         fresh = true;
       }
     }
