@@ -25,11 +25,14 @@ bool FileArray<T>::Map(const std::string &path, uint64_t off, size_t n) {
   struct stat st {};
   const bool ok = fd >= 0 && fstat(fd, &st) == 0;
   if (ok && (uint64_t)st.st_size >= off + bytes) {
-    void *m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+    // only the pages holding [off, off + bytes) (a shard's slice of a chunk)
+    const uint64_t page = (uint64_t)sysconf(_SC_PAGESIZE);
+    const uint64_t first = off / page * page;
+    const size_t len = (size_t)(off + bytes - first);
+    void *m = mmap(nullptr, len, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, (off_t)first);
     if (m != MAP_FAILED) {
-      const size_t len = (size_t)st.st_size;
       hold_ = std::shared_ptr<const void>(m, [len](const void *q) { munmap(const_cast<void *>(q), len); });
-      p_ = reinterpret_cast<const T *>(static_cast<const char *>(m) + off);
+      p_ = reinterpret_cast<const T *>(static_cast<const char *>(m) + (off - first));
       n_ = n;
       close(fd);
       return true;
