@@ -202,3 +202,32 @@ def test_full_workload_matches_reference(name, tmp_path):
     assert text.count(b"\n") == pin["lines"]
     assert _sha(text) == pin["sha256"]
     assert st["queries"] == pin["queries"]
+
+
+@pytest.mark.parametrize("name,world", [("cfg4", 8), ("cfg3", 3)])
+def test_full_workload_sharded_matches_reference(name, world, tmp_path):
+    """The headline workload as the driver's 8-GPU run cuts it: `world` shard
+    sessions (GhostmSessionCreateShard, one after another on this GPU), their
+    outputs concatenated in rank order against the reference CPU program's
+    full output, and their records against the unsharded run's."""
+    pin = _full_pins().get(name)
+    if pin is None:
+        pytest.skip(f"{name} not pinned in full_golden.json")
+    db = workloads.make_db(name, str(tmp_path / "db"))
+    q = workloads.make_queries(name, str(tmp_path / "q"))
+    argv = ["-i", q, "-d", db, "-o", str(tmp_path / "out"), "-D", "0"] + workloads.WORKLOADS[name]["aln"]
+    h = hashlib.sha256()
+    nbytes = 0
+    recs = []
+    for r in range(world):
+        with Session(argv, shard=(r, world)) as s:
+            s.run()
+            text = s.output()
+            h.update(text)
+            nbytes += len(text)
+            recs.append(s.hits())
+    assert nbytes == pin["bytes"]
+    assert h.hexdigest() == pin["sha256"]
+    with Session(argv) as s:
+        s.run()
+        assert np.concatenate(recs).tobytes() == s.hits().tobytes()
