@@ -399,7 +399,8 @@ struct BinTable {
   __device__ uint32_t *Slot(uint32_t k, uint32_t k1, uint32_t m) const {
     return tab + (m < 4 ? k * 4 + m : k1 * 4 + (m - 4));
   }
-  __device__ void Insert(uint32_t b) {
+  // returns the slot index when this call created the bin's slot, else ~0u
+  __device__ uint32_t Insert(uint32_t b) {
     const uint32_t key = Key(b);
     uint32_t k = Bucket(b);
     while (true) {
@@ -408,7 +409,7 @@ struct BinTable {
       const uint32_t mt = Match(sl, key);
       if (mt < 2048u) {
         atomicAdd(Slot(k, k1, mt & 7u), 8u);
-        return;
+        return ~0u;
       }
       const uint32_t e = Empty(sl);
       if (e >= 8) {
@@ -417,15 +418,44 @@ struct BinTable {
       }
       uint32_t *slot = Slot(k, k1, e);
       const uint32_t old = atomicCAS(slot, 0u, key | 8u);
-      if (old == 0) return;
+      if (old == 0) return (uint32_t)(slot - tab);
       if ((old & ~0x7FFu) == key) {
         atomicAdd(slot, 8u);
-        return;
+        return ~0u;
       }
       // another bin took the slot first: look at the same window again
     }
   }
 };
+
+// Emitted bins of query q (total of them in s_emit, any order, all distinct)
+// -> the query's slot in ascending order.
+template <uint32_t BLOCK>
+__device__ __forceinline__ void RankEmitted(const SeedArgs &a, uint32_t q, uint32_t *s_emit, uint32_t total) {
+  const uint32_t tid = threadIdx.x;
+  // pad to a multiple of 16 with values above every bin (ranks unaffected)
+  for (uint32_t e = total + tid; e < ((total + 15) & ~15u); e += BLOCK) s_emit[e] = 0xFFFFFFFFu;
+  __syncthreads();
+  // rank of element e = number of smaller ones; four lanes per element, each
+  // counting a quarter of the array with 128-bit reads
+  uint32_t *os = a.slots + (size_t)q * a.slot_cap;
+  const uint32_t n16 = (total + 15) >> 4;  // 16-element blocks
+  for (uint32_t base4 = 0; base4 < total * 4; base4 += BLOCK) {
+    const uint32_t t4 = base4 + tid;
+    const uint32_t e = t4 >> 2, part = t4 & 3;
+    const uint32_t b = e < total ? s_emit[e] : 0u;
+    uint32_t rank = 0;
+    if (e < total) {
+      for (uint32_t blk = 0; blk < n16; ++blk) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(s_emit + blk * 16 + part * 4);
+        rank += (v.x < b) + (v.y < b) + (v.z < b) + (v.w < b);
+      }
+    }
+    rank += __shfl_xor(rank, 1);
+    rank += __shfl_xor(rank, 2);
+    if (e < total && part == 0) os[rank] = b << a.log_region;
+  }
+}
 
 // Emission from a filled bin table (k_seed_hash, k_seed_filter): the rule
 // (c(b) > 0 or b = 0) and c(b) + c(b+1) >= T per occupied slot, the count to
@@ -474,28 +504,7 @@ __device__ __forceinline__ void EmitFromTable(const SeedArgs &a, uint32_t q, uin
     mask &= mask - 1;
     s_emit[at++] = (s_tab[tid + k * BLOCK] >> 11) - 1;
   }
-  // pad to a multiple of 16 with values above every bin (ranks unaffected)
-  for (uint32_t e = total + tid; e < ((total + 15) & ~15u); e += BLOCK) s_emit[e] = 0xFFFFFFFFu;
-  __syncthreads();
-  // rank of element e = number of smaller ones; four lanes per element, each
-  // counting a quarter of the array with 128-bit reads
-  uint32_t *os = a.slots + (size_t)q * a.slot_cap;
-  const uint32_t n16 = (total + 15) >> 4;  // 16-element blocks
-  for (uint32_t base4 = 0; base4 < total * 4; base4 += BLOCK) {
-    const uint32_t t4 = base4 + tid;
-    const uint32_t e = t4 >> 2, part = t4 & 3;
-    const uint32_t b = e < total ? s_emit[e] : 0u;
-    uint32_t rank = 0;
-    if (e < total) {
-      for (uint32_t blk = 0; blk < n16; ++blk) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(s_emit + blk * 16 + part * 4);
-        rank += (v.x < b) + (v.y < b) + (v.z < b) + (v.w < b);
-      }
-    }
-    rank += __shfl_xor(rank, 1);
-    rank += __shfl_xor(rank, 2);
-    if (e < total && part == 0) os[rank] = b << a.log_region;
-  }
+  RankEmitted<BLOCK>(a, q, s_emit, total);
 }
 
 template <uint32_t BLOCK, uint32_t TSLOTS>
@@ -708,11 +717,50 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
     return;
   }
 
-  // 3. exact counts of the kept entries
+  // 3. exact counts of the kept entries; the lane whose insert created a
+  //    bin's slot remembers it, so step 4 visits each occupied slot once with
+  //    the queue's density (<= QCAP / BLOCK per lane) instead of walking the
+  //    table's TSLOTS / BLOCK slots per lane
+  constexpr uint32_t kQPer = (QCAP + BLOCK - 1) / BLOCK;
   BinTable<TSLOTS> table{s_tab};
-  for (uint32_t k = tid; k < qn; k += BLOCK) table.Insert(s_q[k]);
+  uint32_t made[kQPer];
+#pragma unroll
+  for (uint32_t u = 0; u < kQPer; ++u) {
+    const uint32_t k = tid + u * BLOCK;
+    made[u] = k < qn ? table.Insert(s_q[k]) : kNone;
+  }
   __syncthreads();
-  EmitFromTable<BLOCK, TSLOTS>(a, q, s_tab, s_emit, s_part, &s_total);
+
+  // 4. emission rule per created slot, as EmitFromTable
+  const uint32_t thr = a.threshold;
+  uint32_t mask = 0, mine = 0;
+  bool phantom = false;
+  if (thr != 0) {
+#pragma unroll
+    for (uint32_t u = 0; u < kQPer; ++u) {
+      if (made[u] == kNone) continue;
+      const uint32_t v = s_tab[made[u]];
+      const uint32_t c = (v >> 3) & 0xFFu;
+      if (c >= thr || c + table.Count(v >> 11) >= thr) {  // bin + 1 = v >> 11
+        mask |= 1u << u;
+        ++mine;
+      }
+    }
+    if (tid == 0 && table.Count(0) == 0 && table.Count(1) >= thr) {
+      phantom = true;
+      ++mine;
+    }
+  }
+  const uint32_t base = BlockExclusiveScan(mine, s_part, &s_total);
+  const uint32_t total = s_total;
+  if (tid == 0) a.counts[q] = total;
+  if (total == 0 || total > a.slot_cap) return;  // offset pass redoes the wide ones
+  uint32_t at = base;
+  if (phantom) s_emit[at++] = 0;
+#pragma unroll
+  for (uint32_t u = 0; u < kQPer; ++u)
+    if ((mask >> u) & 1u) s_emit[at++] = (s_tab[made[u]] >> 11) - 1;
+  RankEmitted<BLOCK>(a, q, s_emit, total);
 }
 
 // Slot -> compact copy for queries whose candidates fit their slot.
