@@ -689,23 +689,29 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   __syncthreads();
 
   // 2. filter, then per-wave compaction into the queue
-  auto cell = [&](uint32_t b) { const uint32_t c = b & (FSLOTS - 1); return s_flt[c >> 4] >> ((c & 15) * 2); };
-  uint32_t need = 0, wave_n = 0;
+  //    cells x - 1, x, x + 1 in bits 0-5 from the words holding x - 1 and
+  //    x + 1 (the same word unless the three straddle a word boundary)
+  auto near = [&](uint32_t x) {
+    const uint32_t c0 = (x - 1) & (FSLOTS - 1), c2 = (x + 1) & (FSLOTS - 1);
+    return __builtin_amdgcn_alignbit(s_flt[c2 >> 4], s_flt[c0 >> 4], (c0 & 15) * 2);
+  };
+  uint32_t wave_n = 0;
+  unsigned long long bal[KE];  // wave-uniform: SGPR pairs
 #pragma unroll
   for (uint32_t e = 0; e < KE; ++e) {
     const uint32_t x = bin[e];
     bool nd = false;
-    if (x != kNone) nd = x <= 1 || ((cell(x) >> 1) & 1u) || (cell(x - 1) & 1u) || (cell(x + 1) & 1u);
-    need |= (nd ? 1u : 0u) << e;
-    wave_n += (uint32_t)__popcll(__ballot(nd));
+    if (x != kNone) nd = x <= 1 || (near(x) & 0x19u) != 0;  // seen(x - 1), twice(x), seen(x + 1)
+    bal[e] = __ballot(nd);
+    wave_n += (uint32_t)__popcll(bal[e]);
   }
   uint32_t qbase = 0;
   if (lane == 0) qbase = atomicAdd(&s_qn, wave_n);
   qbase = (uint32_t)__shfl((int)qbase, 0);
 #pragma unroll
   for (uint32_t e = 0; e < KE; ++e) {
-    const bool nd = (need >> e) & 1u;
-    const unsigned long long m = __ballot(nd);
+    const unsigned long long m = bal[e];
+    const bool nd = (m >> lane) & 1ull;
     const uint32_t at = qbase + (uint32_t)__popcll(m & ((1ull << lane) - 1));
     if (nd && at < QCAP) s_q[at] = bin[e];
     qbase += (uint32_t)__popcll(m);
