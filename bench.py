@@ -542,6 +542,9 @@ def main() -> None:
             roof_k1["valu_insts_per_step"] = pmc["k1_valu_insts_per_step"]
             roof_k1["issue_rate_ginst_s"] = rate / 1e9
             roof_k1["frac_of_measured_issue"] = rate / 1e9 / issue["packed_vop3_ginst_s"]
+            if per.get("seed_list_entries"):
+                # wave-instructions per k-mer list entry (a wave-instruction = 64 lane slots)
+                roof_k1["valu_insts_per_list_entry"] = pmc["k1_valu_insts_per_step"] / per["seed_list_entries"]
         out = {
             "metric": "query residues aligned/sec (whole node) + bit-identical hit-list vs CPU",
             "value": total_res / elapsed if ok else None,

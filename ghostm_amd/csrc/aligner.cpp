@@ -1315,6 +1315,7 @@ void Session::Run(bool stream_to_file) {
   stats_.seed_runs_hash = dt.seed_launches_hash;
   stats_.score_rechecks = dt.score_rechecks;
   stats_.seed_bytes = dt.seed_bytes;
+  stats_.seed_list_entries = dt.seed_list_entries;
   stats_.score_cells = dt.score_cells;
   stats_.traceback_cells = dt.traceback_cells;
   stats_.traceback_launches_scan = dt.traceback_launches_scan;

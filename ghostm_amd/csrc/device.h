@@ -66,7 +66,7 @@ struct MergePass {
 
 struct DeviceTimes {
   double seed = 0, score = 0, traceback = 0, merge = 0;  // seconds of device time (HIP events)
-  uint64_t seed_bytes = 0;
+  uint64_t seed_bytes = 0, seed_list_entries = 0;
   uint64_t score_launches = 0, score_launches_packed = 0, score_launches_half = 0;
   uint64_t score_cells = 0, traceback_cells = 0;
   uint64_t traceback_launches = 0, traceback_launches_key = 0;

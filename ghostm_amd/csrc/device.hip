@@ -775,6 +775,7 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
   // algorithmic bytes: query record + 2 CSR words per list + one u32 per
   // position + 8 bytes (start, query) per candidate
   times_.seed_bytes += (uint64_t)nq * (q->L + 8ull * nlists) + bins_total * 4ull + total * 8ull;
+  times_.seed_list_entries += bins_total;
   return total;
 }
 

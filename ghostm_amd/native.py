@@ -76,6 +76,7 @@ class GhostmStats(ctypes.Structure):
         ("seed_filter_overflows", c_uint64),
         ("score_launches_swar", c_uint64),
         ("traceback_launches_scan_swar", c_uint64),
+        ("seed_list_entries", c_uint64),
     ]
 
     def as_dict(self) -> dict:
