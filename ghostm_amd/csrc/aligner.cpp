@@ -19,6 +19,7 @@
 #include <stdexcept>
 
 #include "common.h"
+#include "worker_pool.h"
 
 namespace ghostm {
 
@@ -88,6 +89,7 @@ unsigned HostThreads() {
   return std::max(1u, std::min(share, 16u));
 }
 
+
 void ParallelFor(size_t n, unsigned threads,
                  const std::function<void(size_t, size_t, unsigned)> &fn) {
   if (n == 0) return;
@@ -96,23 +98,9 @@ void ParallelFor(size_t n, unsigned threads,
     fn(0, n, 0);
     return;
   }
-  std::vector<std::thread> pool;
-  std::vector<std::exception_ptr> errors(threads);
   const size_t per = (n + threads - 1) / threads;
-  for (unsigned t = 0; t < threads; ++t) {
-    const size_t b = t * per, e = std::min(n, b + per);
-    if (b >= e) break;
-    pool.emplace_back([&fn, &errors, b, e, t] {
-      try {
-        fn(b, e, t);
-      } catch (...) {
-        errors[t] = std::current_exception();
-      }
-    });
-  }
-  for (auto &th : pool) th.join();
-  for (auto &ep : errors)
-    if (ep) std::rethrow_exception(ep);
+  const unsigned pieces = (unsigned)((n + per - 1) / per);
+  WorkerPool::Get().Run(pieces, [&](unsigned t) { fn(t * per, std::min(n, (size_t)t * per + per), t); });
 }
 
 // ------------------------------------------------------------------ TaskQueue
