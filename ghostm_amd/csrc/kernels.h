@@ -2705,27 +2705,25 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
       return in ? x : kSeqEnd;
     };
     auto fetch_raw = [&](uint32_t jn, uint32_t p0, uint32_t cl) -> uint32_t { return a.db[p0 - min(jn, cl)]; };
-    uint32_t nA = fetch(-(int)i, p0A, wA), nB = fetch(-(int)i, p0B, wB);           // this column
-    uint32_t mA = fetch(1 - (int)i, p0A, wA), mB = fetch(1 - (int)i, p0B, wB);     // the next one
+    // residues by step parity: slot P holds the code of the next step of
+    // parity P. A step reads its slot and refills it for step + 2, so the
+    // loads land where they are read (no register rotation, no copy of a load
+    // result that would wait for it); the loops run steps in pairs
+    uint32_t cA[2] = {fetch(-(int)i, p0A, wA), fetch(1 - (int)i, p0A, wA)};
+    uint32_t cB[2] = {fetch(-(int)i, p0B, wB), fetch(1 - (int)i, p0B, wB)};
     const typename C::Step st_run = cell.At(0u, 0u);  // no END in this column or the one before
-    auto column = [&](uint32_t step, auto run_c) {
+    auto column = [&](uint32_t step, auto run_c, auto par_c) {
       constexpr bool run = decltype(run_c)::value;
+      constexpr int P = decltype(par_c)::value;
       const int j = (int)step - (int)i;
       uint32_t hin = ShiftUp(hout), fin = ShiftUp(fout);
       if (i == 0) { hin = sig; fin = 0; }  // framed 0 is a real F <= 0
       const uint32_t diag0 = hprev;
       hprev = hin;
-      const uint32_t rA = nA, rB = nB;
-      nA = mA;
-      nB = mB;
+      const uint32_t rA = cA[P], rB = cB[P];
       uint32_t end = 0;
       typename C::Step st = st_run;
-      if constexpr (run) {
-        mA = fetch_raw((uint32_t)(j + 2), p0A, clA);
-        mB = fetch_raw((uint32_t)(j + 2), p0B, clB);
-      } else {
-        mA = fetch(j + 2, p0A, wA);
-        mB = fetch(j + 2, p0B, wB);
+      if constexpr (!run) {
         // END halves: codes are 0..25 with END = 25 the largest
         end = PkSign(PkAddU16(rA | (rB << 16), 0x7FE77FE7u));
         if (j >= 0) dead |= end;                  // the reference breaks at END
@@ -2734,10 +2732,18 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
           prev_end = end;
         }
       }
-      const hf2 Z1 = SWAR ? HF(sig + EXTP) : HF(W(HF(sig) + HF(EXTP)));  // FRAMED: the next column's frame
-      const hf2 KOE = HF(Cells<true>::Pair(a.open - a.ext)), NEXT = HF(Cells<true>::Pair(a.ext));
       const uint32_t cbase = MadU24(min(rA, kPairCodes - 1), kPairCodes * kPairStride * 4,
                                     MulU24(min(rB, kPairCodes - 1), kPairStride * 4));
+      // the residues two columns ahead, into this step's slot once rA/rB are used
+      if constexpr (run) {
+        cA[P] = fetch_raw((uint32_t)(j + 2), p0A, clA);
+        cB[P] = fetch_raw((uint32_t)(j + 2), p0B, clB);
+      } else {
+        cA[P] = fetch(j + 2, p0A, wA);
+        cB[P] = fetch(j + 2, p0B, wB);
+      }
+      const hf2 Z1 = SWAR ? HF(sig + EXTP) : HF(W(HF(sig) + HF(EXTP)));  // FRAMED: the next column's frame
+      const hf2 KOE = HF(Cells<true>::Pair(a.open - a.ext)), NEXT = HF(Cells<true>::Pair(a.ext));
       const char *tp = reinterpret_cast<const char *>(s_pair) + cbase;
       auto T = [&](int u) { return *reinterpret_cast<const uint32_t *>(tp + ((qoff[u >> 2] >> (8 * (u & 3))) & 0xFFu)); };
       uint32_t diag = diag0, F = fin, cm = sig;
@@ -2819,11 +2825,23 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
     };
     // EXACT windows (cut at the subject's start) meet no END inside; the first
     // G steps still hold the fill columns and each lane's first column
+    using P0 = std::integral_constant<int, 0>;
+    using P1 = std::integral_constant<int, 1>;
     uint32_t step = 0;
     const uint32_t general = EXACT ? min(a.G, steps) : steps;
-    for (; step < general; ++step) column(step, std::false_type{});
-    if constexpr (EXACT)
-      for (; step < steps; ++step) column(step, std::true_type{});
+    for (; step + 1 < general; step += 2) {
+      column(step, std::false_type{}, P0{});
+      column(step + 1, std::false_type{}, P1{});
+    }
+    if (step < general) column(step++, std::false_type{}, P0{});
+    if constexpr (EXACT) {
+      if ((step & 1) && step < steps) column(step++, std::true_type{}, P1{});
+      for (; step + 1 < steps; step += 2) {
+        column(step, std::true_type{}, P0{});
+        column(step + 1, std::true_type{}, P1{});
+      }
+      if (step < steps) column(step++, std::true_type{}, P0{});
+    }
     int BA = SWAR ? (int)(best & 0xFFFFu) : C::Decode(best & 0xFFFFu), CA = (int)(col & 0xFFFFu);
     int BB = SWAR ? (int)(best >> 16) : C::Decode(best >> 16), CB = (int)(col >> 16);
     // first column over the group's row strips
