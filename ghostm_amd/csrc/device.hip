@@ -1288,6 +1288,7 @@ void DeviceModule::MergeLaunch(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, 
   if (ng == 0) return;
   if (d->nsubj == 0) throw Error("DB subjects not set for the device merge");
   const size_t slots = (size_t)ng * cap;
+  if (slots >= (1ull << 32)) throw Error("too many result slots in one segment (groups x -b >= 2^32)");
   const bool carry_in = pass.carry_in, carry_out = pass.carry_out;
   if ((carry_in || carry_out) && I.carry_count.bytes < (size_t)q->ngroups * 4)
     throw Error("ResetCarry was not called for this query chunk");

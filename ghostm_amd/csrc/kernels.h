@@ -2323,10 +2323,12 @@ __global__ void k_finalize(const uint32_t *sel_count, const uint32_t *sel_score,
                            const uint32_t *subj_start, uint32_t ng, uint32_t cap, uint32_t chunk,
                            const uint32_t *sel_from, const SlotHit *carry, SlotHit *out,
                            unsigned long long *traced) {
-  const size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ uint32_t s_fresh;
+  if (threadIdx.x == 0) s_fresh = 0;
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;  // slots = ng * cap < 2^32
   bool fresh = false;  // a hit of this pass's candidates, traced back by K3
-  if (s < (size_t)ng * cap) {
-    const uint32_t g = (uint32_t)(s / cap), k = (uint32_t)(s - (size_t)g * cap);
+  if (s < ng * cap) {
+    const uint32_t g = s / cap, k = s - g * cap;
     if (k < sel_count[g]) {
       if (sel_from && sel_from[s] != kNoSlot) {
         out[s] = carry[(size_t)g * cap + sel_from[s]];
@@ -2337,7 +2339,13 @@ __global__ void k_finalize(const uint32_t *sel_count, const uint32_t *sel_score,
       }
     }
   }
-  WaveAddCells(traced, fresh ? 1ull : 0ull);
+  // one global atomic per workgroup (every wave adding to one address
+  // serialised them in the L2)
+  __syncthreads();
+  const uint32_t n = (uint32_t)__popcll(__ballot(fresh));
+  if ((threadIdx.x & 63) == 0 && n) atomicAdd(&s_fresh, n);
+  __syncthreads();
+  if (threadIdx.x == 0 && s_fresh && traced) atomicAdd(traced, (unsigned long long)s_fresh);
 }
 
 // The gathered hit record (include/ghostm_hip.h GhostmHit), written on the
