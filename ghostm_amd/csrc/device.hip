@@ -130,7 +130,7 @@ struct DeviceModule::Impl {
   struct Prepared {
     bool valid = false;
     uint64_t cand_begin = 0, n = 0;
-    uint32_t count = 0, per_block = 0;
+    uint32_t count = 0, per_block = 0, qmax = 0;
     int buf = 0;
   } prepared;
   struct ScoreState {                       // the launched, not yet finished K2
@@ -793,12 +793,12 @@ void DeviceModule::CopyStarts(uint64_t begin, uint64_t n, uint32_t *out) {
 // written straight into page-locked staging (no fresh host vector per segment:
 // its first touch cost more than the loop). A task closes when full, when it
 // spans Qmax queries, or at the end, so ScoreTaskBound is an upper bound.
-static size_t ScoreTaskBound(uint64_t n, uint32_t q_first, uint32_t q_end, uint32_t per_block) {
-  return (size_t)(n / per_block) + (q_end - q_first) / kern::kScoreQmax + 2;
+static size_t ScoreTaskBound(uint64_t n, uint32_t q_first, uint32_t q_end, uint32_t per_block, uint32_t qmax) {
+  return (size_t)(n / per_block) + (q_end - q_first) / qmax + 2;
 }
 static size_t BuildScoreTasks(uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32_t q_end,
                               const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets,
-                              uint32_t per_block, kern::ScoreTask *out) {
+                              uint32_t per_block, uint32_t qmax, kern::ScoreTask *out) {
   size_t nt = 0;
   kern::ScoreTask cur{};
   bool open_task = false;
@@ -811,7 +811,7 @@ static size_t BuildScoreTasks(uint64_t cand_begin, uint64_t n, uint32_t q_first,
     uint64_t lo = std::max<uint64_t>(offsets[qi], cand_begin);
     const uint64_t hi = std::min<uint64_t>(offsets[qi] + counts[qi], cand_end);
     while (lo < hi) {
-      if (open_task && (cur.count == per_block || qi - cur.q_first >= (uint32_t)kern::kScoreQmax)) flush();
+      if (open_task && (cur.count == per_block || qi - cur.q_first >= qmax)) flush();
       if (!open_task) {
         cur = kern::ScoreTask{};
         cur.begin = lo;
@@ -826,6 +826,21 @@ static size_t BuildScoreTasks(uint64_t cand_begin, uint64_t n, uint32_t q_first,
   }
   flush();
   return nt;
+}
+
+// k_score16f's unit-pair kernel (UNIT) holds the profiles of kScoreQmaxUnit
+// queries per block instead of kScoreQmax: used where a segment averages at
+// least 80 candidates per query, so that two queries still fill a block's 128
+// candidate slots (a simulation with Poisson counts: 8 % more non-empty waves
+// than with 4 queries per block at 63 per query, 5.6 % at 80, 0.3 % at 127;
+// cfg 4 averages 127, cfg 3 63). GHOSTM_K2=unit forces it, swar16 keeps the
+// 16-bit profile kernel.
+static bool ScoreUnit(bool swar, uint64_t n, uint32_t q_first, uint32_t q_end) {
+  if (!swar) return false;
+  const char *force = getenv("GHOSTM_K2");
+  if (force && strcmp(force, "unit") == 0) return true;
+  if (force && strcmp(force, "swar16") == 0) return false;
+  return q_end > q_first && n >= (uint64_t)80 * (q_end - q_first);
 }
 
 // the packed K2 encodings (two candidates per lane) whenever every value fits
@@ -887,12 +902,14 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
   int guard = swar ? 0 : framed ? (bound + sigma_max < 2040 ? 0 : (int)(2040 - sigma_max)) : (bound < 2048 ? 0 : 2000);
   if (half && getenv("GHOSTM_K2_GUARD")) guard = atoi(getenv("GHOSTM_K2_GUARD"));  // tests: force re-scores
   const uint32_t per_block = ScorePerBlock(q, base, gap);
+  const bool unit = ScoreUnit(swar, n, q_first, q_end);
+  const uint32_t qmax = unit ? kern::kScoreQmaxUnit : kern::kScoreQmax;
   // tasks: prepared for this range by the previous launch (uploaded on the copy
   // stream into the other task buffer), else built and uploaded here
   int buf = -1;
   size_t ntasks = 0;
   if (I.prepared.valid && I.prepared.cand_begin == cand_begin && I.prepared.n == n &&
-      I.prepared.per_block == per_block) {
+      I.prepared.per_block == per_block && I.prepared.qmax == qmax) {
     buf = I.prepared.buf;
     ntasks = I.prepared.count;
     HIP_CHECK(hipStreamWaitEvent(S(stream_), I.ev_tasks, 0));
@@ -905,8 +922,9 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
     // page-locked staging per task buffer: this one's last upload was read by
     // a launch that has been waited for, so the copy needs no wait either
     PinnedBuf &hs = I.h_tasks[buf];
-    hs.Reserve(ScoreTaskBound(n, q_first, q_end, per_block) * sizeof(kern::ScoreTask));
-    ntasks = BuildScoreTasks(cand_begin, n, q_first, q_end, counts, offsets, per_block, hs.as<kern::ScoreTask>());
+    hs.Reserve(ScoreTaskBound(n, q_first, q_end, per_block, qmax) * sizeof(kern::ScoreTask));
+    ntasks = BuildScoreTasks(cand_begin, n, q_first, q_end, counts, offsets, per_block, qmax,
+                             hs.as<kern::ScoreTask>());
     TraceMark("tasks", ntasks);
     const size_t tb = ntasks * sizeof(kern::ScoreTask);
     I.task_buf[buf].Reserve(tb);
@@ -949,26 +967,31 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
     a.guard_list = I.guard_list.as<uint32_t>();
   }
   // packed: the profiles, then the 32 x 32 code table they are built from
-  const size_t lds = packed ? (size_t)kern::kScoreQmax * kern::kProfRows16 * (lay.Lpad + 8) * 2 + 32 * 32 * 2
-                            : (size_t)kern::kScoreQmax * kern::kProfRows * (lay.Lpad + 4) * 4;
+  // (UNIT: 32-bit words, rows padded by 4 words, a 32 x 32 word code table)
+  const size_t lds = unit     ? (size_t)kern::kScoreQmaxUnit * kern::kProfRows16 * (lay.Lpad + 4) * 4 + 32 * 32 * 4
+                     : packed ? (size_t)kern::kScoreQmax * kern::kProfRows16 * (lay.Lpad + 8) * 2 + 32 * 32 * 2
+                              : (size_t)kern::kScoreQmax * kern::kProfRows * (lay.Lpad + 4) * 4;
   HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
   const dim3 grid((uint32_t)ntasks), block(kern::kScoreBlock);
   if (packed) {
     switch (lay.S) {
       case 32:
-        if (swar) hipLaunchKernelGGL((kern::k_score16f<32, true>), grid, block, lds, S(stream_), a);
+        if (unit) hipLaunchKernelGGL((kern::k_score16f<32, true, true>), grid, block, lds, S(stream_), a);
+        else if (swar) hipLaunchKernelGGL((kern::k_score16f<32, true>), grid, block, lds, S(stream_), a);
         else if (framed) hipLaunchKernelGGL((kern::k_score16f<32>), grid, block, lds, S(stream_), a);
         else if (half) hipLaunchKernelGGL((kern::k_score16<32, true>), grid, block, lds, S(stream_), a);
         else hipLaunchKernelGGL((kern::k_score16<32, false>), grid, block, lds, S(stream_), a);
         break;
       case 16:
-        if (swar) hipLaunchKernelGGL((kern::k_score16f<16, true>), grid, block, lds, S(stream_), a);
+        if (unit) hipLaunchKernelGGL((kern::k_score16f<16, true, true>), grid, block, lds, S(stream_), a);
+        else if (swar) hipLaunchKernelGGL((kern::k_score16f<16, true>), grid, block, lds, S(stream_), a);
         else if (framed) hipLaunchKernelGGL((kern::k_score16f<16>), grid, block, lds, S(stream_), a);
         else if (half) hipLaunchKernelGGL((kern::k_score16<16, true>), grid, block, lds, S(stream_), a);
         else hipLaunchKernelGGL((kern::k_score16<16, false>), grid, block, lds, S(stream_), a);
         break;
       default:
-        if (swar) hipLaunchKernelGGL((kern::k_score16f<8, true>), grid, block, lds, S(stream_), a);
+        if (unit) hipLaunchKernelGGL((kern::k_score16f<8, true, true>), grid, block, lds, S(stream_), a);
+        else if (swar) hipLaunchKernelGGL((kern::k_score16f<8, true>), grid, block, lds, S(stream_), a);
         else if (framed) hipLaunchKernelGGL((kern::k_score16f<8>), grid, block, lds, S(stream_), a);
         else if (half) hipLaunchKernelGGL((kern::k_score16<8, true>), grid, block, lds, S(stream_), a);
         else hipLaunchKernelGGL((kern::k_score16<8, false>), grid, block, lds, S(stream_), a);
@@ -988,6 +1011,7 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
   times_.score_launches_half += half ? 1 : 0;
   times_.score_launches_framed += framed ? 1 : 0;
   times_.score_launches_swar += swar ? 1 : 0;
+  times_.score_launches_unit += unit ? 1 : 0;
   P.active = true;
   P.guarded = half && guard;
   P.cand_begin = cand_begin;
@@ -1001,14 +1025,16 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
   if (next && next->n) {
     const int nb = I.task_turn;
     PinnedBuf &hs = I.h_tasks[nb];
-    hs.Reserve(ScoreTaskBound(next->n, next->q_first, next->q_end, per_block) * sizeof(kern::ScoreTask));
+    const uint32_t nqmax = ScoreUnit(swar, next->n, next->q_first, next->q_end) ? kern::kScoreQmaxUnit
+                                                                                 : kern::kScoreQmax;
+    hs.Reserve(ScoreTaskBound(next->n, next->q_first, next->q_end, per_block, nqmax) * sizeof(kern::ScoreTask));
     const size_t nt = BuildScoreTasks(next->cand_begin, next->n, next->q_first, next->q_end, counts, offsets,
-                                      per_block, hs.as<kern::ScoreTask>());
+                                      per_block, nqmax, hs.as<kern::ScoreTask>());
     I.task_buf[nb].Reserve(nt * sizeof(kern::ScoreTask));
     HIP_CHECK(hipMemcpyAsync(I.task_buf[nb].p, hs.p, nt * sizeof(kern::ScoreTask), hipMemcpyHostToDevice,
                              S(copy_stream_)));
     HIP_CHECK(hipEventRecord(I.ev_tasks, S(copy_stream_)));
-    I.prepared = Impl::Prepared{true, next->cand_begin, next->n, (uint32_t)nt, per_block, nb};
+    I.prepared = Impl::Prepared{true, next->cand_begin, next->n, (uint32_t)nt, per_block, nqmax, nb};
   }
 }
 

@@ -793,6 +793,7 @@ __device__ inline void WaveAddCells(unsigned long long *counter, unsigned long l
 // ------------------------------------------------------------------ K2 score
 constexpr int kScoreBlock = 256;
 constexpr int kScoreQmax = 4;
+constexpr int kScoreQmaxUnit = 2;  // k_score16f UNIT: 32-bit profile words, half the queries per block
 constexpr uint32_t kProfRows = 26;
 constexpr uint32_t kProfRows16 = 32;  // packed kernels: one profile row per residue code
 constexpr uint32_t kFillCode = 26;     // k_score16f: profile row of the columns before the window
@@ -1060,6 +1061,18 @@ template <> struct Cells<true> {
   }
 };
 
+// Unit-pair diagonal sum (k_score16f UNIT): a = (vA, 1), b = (vB, 1) as (lo, hi)
+// halves. One v_pk_mad_u16 whose op_sel swaps b's halves:
+// lo = vA * 1 + h.lo, hi = 1 * vB + h.hi (per half modulo 2^16).
+// (b passes through an empty asm: straight from a ds_read_b128 tuple's first
+// register the compiler rotated it with a v_alignbit_b32 instead of op_sel;
+// a real inline-asm mad costs a conservative s_nop after every one)
+__device__ inline uint32_t PkMadUnit(uint32_t a, uint32_t b, uint32_t h) {
+  asm("" : "+v"(b));
+  const us2 bs = __builtin_shufflevector(U2(b), U2(b), 1, 0);
+  return W(U2(a) * bs + U2(h));
+}
+
 __device__ inline uint32_t MadU24(uint32_t a, uint32_t b, uint32_t c) {
   uint32_t r;
   asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
@@ -1133,6 +1146,44 @@ __device__ __forceinline__ void BuildProfile16(const ScoreArgs &a, const ScoreTa
     }
 #pragma unroll
     for (int c = 0; c < 32; ++c) dst[c * RS] = (short)((c & 1) ? w[c >> 1] >> 16 : w[c >> 1]);
+  }
+}
+
+// The same profiles as BuildProfile16<C, true, true> (SWAR values), each entry a
+// 32-bit unit-pair word (v, 1) for k_score16f's UNIT kernel: slot-major, 32
+// code rows of RS words per slot, the 32 x 32 word code table behind the
+// kScoreQmaxUnit slots.
+__device__ __forceinline__ void BuildProfileUnit(const ScoreArgs &a, const ScoreTask &t, uint32_t *s_prof32,
+                                                 uint32_t RS) {
+  uint32_t *s_enc = s_prof32 + kScoreQmaxUnit * kProfRows16 * RS;
+  const int extp = -a.ext;
+  const uint32_t drop = (uint32_t)(0x10000u - (a.swar_low - 64u)) & 0xFFFFu;
+  for (uint32_t e = threadIdx.x; e < 32 * 32; e += kScoreBlock) {
+    const uint32_t q = e >> 5, c = e & 31;
+    const int v = c < 25 ? a.mat[c * 32 + q] : 0;
+    const uint32_t v16 = c < kSeqEnd ? (uint32_t)(v + extp) & 0xFFFFu : c == kSeqEnd ? a.swar_restart : drop;
+    s_enc[e] = v16 | 0x10000u;
+  }
+  __syncthreads();
+  const uint32_t rows = t.q_count * a.Lpad;
+  for (uint32_t p = threadIdx.x; p < rows; p += kScoreBlock) {
+    const uint32_t slot = p / a.Lpad, r = p - slot * a.Lpad;
+    uint32_t *dst = s_prof32 + slot * kProfRows16 * RS + r;
+    if (r < a.pad) {
+#pragma unroll
+      for (int c = 0; c < 32; ++c) dst[c * RS] = (c == (int)kSeqEnd ? a.swar_restart : drop) | 0x10000u;
+    } else {
+      const uint32_t q = a.qseq[(size_t)(t.q_first + slot) * a.L + (r - a.pad)];
+      const uint4 *src = reinterpret_cast<const uint4 *>(s_enc + q * 32);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint4 v = src[k];
+        dst[(4 * k) * RS] = v.x;
+        dst[(4 * k + 1) * RS] = v.y;
+        dst[(4 * k + 2) * RS] = v.z;
+        dst[(4 * k + 3) * RS] = v.w;
+      }
+    }
   }
 }
 
@@ -1339,15 +1390,34 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16(ScoreArgs a) {
 // mask m = 0 applies there and the END profile row holds swar_restart, so every
 // row of the END column comes out as real 0 (h = swar_restart; a later END first
 // clears E where the half already met one). The column after it is ordinary.
-template <int S, bool SWAR = false>
-__global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
+//
+// UNIT = true (with SWAR; k_score16f<S, true, true>): unit-pair profile words.
+// Every profile entry is a 32-bit word (v, 1): the 16-bit SWAR value in the low
+// half and the constant 1 in the high half (BuildProfileUnit). The diagonal term
+// of a row is then ONE v_pk_mad_u16 with op_sel instead of a v_perm_b32 that
+// pairs the two candidates' values plus a v_pk_mad_u16:
+//   lo = A.lo * B.hi + H.lo = vA * 1 + H.lo,   hi = A.hi * B.lo + H.hi = 1 * vB + H.hi
+// (per half modulo 2^16, as before). The END column's diagonal mask (m = 0 in
+// the END halves) becomes an AND of the previous column's H in those halves,
+// done in place before the rows, only on steps where some lane meets END. The
+// words take twice the LDS of the 16-bit rows, so a block holds the profiles
+// of at most kScoreQmaxUnit queries (the host uses this kernel when a segment
+// averages enough candidates per query to fill its blocks).
+template <int S, bool SWAR = false, bool UNIT = false>
+__global__ __launch_bounds__(kScoreBlock, 4) void k_score16f(ScoreArgs a) {  // 4 waves per SIMD: <= 128 VGPRs
+  static_assert(!UNIT || SWAR, "unit-pair words carry integer patterns");
   using C = Cells<true>;
   extern __shared__ __attribute__((aligned(16))) short s_prof16[];
   const ScoreTask t = a.tasks[blockIdx.x];
-  const uint32_t RS = a.Lpad + 8;
+  // UNIT: row stride in 32-bit words (4-word pad), else in 16-bit elements
+  const uint32_t RS = UNIT ? a.Lpad + 4 : a.Lpad + 8;
   const int extp = -a.ext;
 
-  BuildProfile16<C, true, SWAR>(a, t, s_prof16, RS);  // row kFillCode: the columns before the window
+  // row kFillCode: the columns before the window
+  if constexpr (UNIT)
+    BuildProfileUnit(a, t, reinterpret_cast<uint32_t *>(s_prof16), RS);
+  else
+    BuildProfile16<C, true, SWAR>(a, t, s_prof16, RS);
   __syncthreads();
 
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1356,6 +1426,8 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
   const bool in_group = g < a.gpw;
   const bool vA = in_group && 2 * pair < t.count;
   const bool vB = in_group && 2 * pair + 1 < t.count;
+  // a wave past the task's last candidate has nothing to do (no barrier follows)
+  if (!__builtin_amdgcn_ballot_w64(vA)) return;
   const unsigned long long cA = t.begin + 2 * pair, cB = cA + 1;
   uint32_t slotA = 0, slotB = 0, offA = 0, offB = 0, wA = 0, wB = 0;
   if (vA) {
@@ -1376,12 +1448,13 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   typedef __attribute__((address_space(3))) const u32x4 lds_u4;
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char *)s_prof16;
-  const uint32_t baseA2 = lds0 + (slotA * kProfRows16 * RS + i * S) * 2;
-  const uint32_t baseB2 = lds0 + (slotB * kProfRows16 * RS + i * S) * 2;
+  constexpr uint32_t EB = UNIT ? 4 : 2;  // bytes per profile entry
+  const uint32_t baseA2 = lds0 + (slotA * kProfRows16 * RS + i * S) * EB;
+  const uint32_t baseB2 = lds0 + (slotB * kProfRows16 * RS + i * S) * EB;
   const uint8_t *dbp = a.db - kDbFrontPad;
   const uint32_t back = kDbFrontPad + a.dblen;
   const uint32_t xA = (vA ? offA + kDbFrontPad : back) - i, xB = (vB ? offB + kDbFrontPad : back) - i;
-  const uint32_t RS2 = RS * 2;
+  const uint32_t RS2 = RS * EB;
   // the padded DB as a raw buffer (gfx9 descriptor word 3; every access stays
   // inside the padding, so the range is left open)
   const __amdgpu_buffer_rsrc_t dbr = __builtin_amdgcn_make_buffer_rsrc((void *)dbp, 0, 0x7FFFFFFF, 0x00020000);
@@ -1481,6 +1554,15 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
 #pragma unroll
           for (int k = 0; k < S; ++k) E[k] = BfiV(reset, 0u, E[k]);
         }
+        if constexpr (UNIT) {
+          // the diagonal mask: the previous column's H reads as 0 in the END
+          // halves (only the diagonal sums read the old H before the rows
+          // overwrite it; the row above's hand-over through hprev likewise)
+          const uint32_t keep = ~end;
+#pragma unroll
+          for (int k = 0; k < S; ++k) H[k] &= keep;
+          hprev &= keep;
+        }
       }
     }
     if (i == 0) { hin = sigc; fin = NEGF; }  // real 0 for H; any real F <= 0 will do
@@ -1497,19 +1579,56 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
       if constexpr (SWAR) return W(U2(h) * U2(mreg) + U2(p));  // v_pk_mad_u16
       else return C::Diag(h, m, p);
     };
+    // UNIT: the words of rows k..k+3 / k+4..k+7 (the next chunk's are loaded
+    // into them as soon as the current chunk's diagonal sums have read them)
+#ifndef GHOSTM_K2_PREFETCH
+#define GHOSTM_K2_PREFETCH 1
+#endif
+    constexpr bool PF = UNIT && GHOSTM_K2_PREFETCH;
+    u32x4 ua0{}, ua1{}, ub0{}, ub1{};
+    if constexpr (UNIT) {
+      ua0 = pA[0];
+      ub0 = pB[0];
+      ua1 = pA[1];
+      ub1 = pB[1];
+    }
 #pragma unroll
     for (int k = 0; k < S; k += 8) {
-      const u32x4 qa = pA[k / 8];
-      const u32x4 qb = pB[k / 8];
-      const uint32_t wa[4] = {qa.x, qa.y, qa.z, qa.w}, wb[4] = {qb.x, qb.y, qb.z, qb.w};
+      uint32_t wa[8], wb[8];  // UNIT: one word per row; else two rows per word
+      if constexpr (UNIT) {
+        if constexpr (!PF) {
+          if (k > 0) {
+            ua0 = pA[k / 4];
+            ub0 = pB[k / 4];
+            ua1 = pA[k / 4 + 1];
+            ub1 = pB[k / 4 + 1];
+          }
+        }
+        const u32x4 qa0 = ua0, qa1 = ua1;
+        const u32x4 qb0 = ub0, qb1 = ub1;
+        wa[0] = qa0.x; wa[1] = qa0.y; wa[2] = qa0.z; wa[3] = qa0.w;
+        wa[4] = qa1.x; wa[5] = qa1.y; wa[6] = qa1.z; wa[7] = qa1.w;
+        wb[0] = qb0.x; wb[1] = qb0.y; wb[2] = qb0.z; wb[3] = qb0.w;
+        wb[4] = qb1.x; wb[5] = qb1.y; wb[6] = qb1.z; wb[7] = qb1.w;
+      } else {
+        const u32x4 qa = pA[k / 8];
+        const u32x4 qb = pB[k / 8];
+        wa[0] = qa.x; wa[1] = qa.y; wa[2] = qa.z; wa[3] = qa.w;
+        wb[0] = qb.x; wb[1] = qb.y; wb[2] = qb.z; wb[3] = qb.w;
+      }
       // row u's profile pair (perm) and diagonal sum, formed from the previous
       // column's H[k + u - 1] before row u - 1 overwrites it
       auto prof = [&](int u) {
-        return __builtin_amdgcn_perm(wb[u >> 1], wa[u >> 1], (u & 1) ? 0x07060302u : 0x05040100u);
+        if constexpr (UNIT) return 0u;  // unused: the words go straight into the mad
+        else return __builtin_amdgcn_perm(wb[u >> 1], wa[u >> 1], (u & 1) ? 0x07060302u : 0x05040100u);
+      };
+      auto dsum = [&](uint32_t h, int u, uint32_t p) -> uint32_t {
+        if constexpr (UNIT) return PkMadUnit(wa[u], wb[u], h);
+        else return diag_sum(h, p);
       };
       uint32_t s[8];
-      s[0] = diag_sum(diag, prof(0));
-      s[1] = diag_sum(H[k], prof(1));
+      s[0] = dsum(diag, 0, prof(0));
+      s[1] = dsum(H[k], 1, prof(1));
       diag = H[k + 7];
       // row u + 2's perm and diagonal sum and row u's E update sit between the
       // dependent steps h -> oE -> max -> F, so few packed ops read the result
@@ -1521,7 +1640,17 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
         if (u + 2 < 8) p2 = prof(u + 2);
         H[k + u] = W(h);
         const hf2 oE = SWAR ? HF(W(h) + KOE32) : h + KOE;
-        if (u + 2 < 8) s[u + 2] = diag_sum(H[k + u + 1], p2);
+        if (u + 2 < 8) s[u + 2] = dsum(H[k + u + 1], u + 2, p2);
+        if constexpr (PF) {
+          if (u == 1 && k + 8 < S) {  // rows k..k+3 read: the next chunk's first four
+            ua0 = pA[k / 4 + 2];
+            ub0 = pB[k / 4 + 2];
+          }
+          if (u == 5 && k + 8 < S) {  // rows k+4..k+7 read
+            ua1 = pA[k / 4 + 3];
+            ub1 = pB[k / 4 + 3];
+          }
+        }
         const hf2 G = __builtin_elementwise_maximum(HF(F), oE);
         E[k + u] = W(__builtin_elementwise_maximum(__builtin_elementwise_maximum(HF(E[k + u]), oE), Z1));
         F = SWAR ? W(G) + NEXT32 : W(G + NEXT);

@@ -206,7 +206,8 @@ def test_reference_gpu_batching_rule(dataset):
     lib.FreeGpu()
 
 
-@pytest.mark.parametrize("kind", ["int32", "int16", "f16plain", "f16frame", "k2_nowait", "k3_int32", "k1_merge"])
+@pytest.mark.parametrize("kind", ["int32", "int16", "f16plain", "f16frame", "swar16", "unit", "k2_nowait", "k3_int32",
+                                  "k1_merge"])
 @pytest.mark.parametrize("ds,var,opts", [("syn_small", "default", []), ("syn_short", "default", []),
                                          ("syn_small", "r64_pam250", ["-r", "64", "-M", cases.PAM250, "-y", "2"])])
 def test_forced_score_encoding_matches_golden(kind, ds, var, opts, dataset, golden, tmp_path):
@@ -231,6 +232,10 @@ def test_forced_score_encoding_matches_golden(kind, ds, var, opts, dataset, gold
         assert st["score_launches_half"] == st["score_launches"] > 0 and st["score_launches_framed"] == 0
     elif kind == "f16frame":  # the f16-number frame (k_score16f<S, false>), guarded where needed
         assert st["score_launches_framed"] == st["score_launches"] > 0 and st["score_launches_swar"] == 0
+    elif kind == "swar16":  # integer patterns with 16-bit profile rows (k_score16f<S, true>)
+        assert st["score_launches_swar"] == st["score_launches"] > 0 and st["score_launches_unit"] == 0
+    elif kind == "unit":  # ... with unit-pair profile words (k_score16f<S, true, true>), however sparse
+        assert st["score_launches_unit"] == st["score_launches"] > 0
     else:
         assert st["score_launches"] > 0 and st["score_launches_half"] == 0
         assert st["score_launches_packed"] == (st["score_launches"] if kind == "int16" else 0)
