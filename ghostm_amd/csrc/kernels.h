@@ -1161,7 +1161,8 @@ __device__ __forceinline__ void BuildProfileUnit(const ScoreArgs &a, const Score
   for (uint32_t e = threadIdx.x; e < 32 * 32; e += kScoreBlock) {
     const uint32_t q = e >> 5, c = e & 31;
     const int v = c < 25 ? a.mat[c * 32 + q] : 0;
-    const uint32_t v16 = c < kSeqEnd ? (uint32_t)(v + extp) & 0xFFFFu : c == kSeqEnd ? a.swar_restart : drop;
+    // END reads the drop as well: its column comes out as RESTART through E (k_score16f UNIT)
+    const uint32_t v16 = c < kSeqEnd ? (uint32_t)(v + extp) & 0xFFFFu : drop;
     s_enc[e] = v16 | 0x10000u;
   }
   __syncthreads();
@@ -1171,7 +1172,7 @@ __device__ __forceinline__ void BuildProfileUnit(const ScoreArgs &a, const Score
     uint32_t *dst = s_prof32 + slot * kProfRows16 * RS + r;
     if (r < a.pad) {
 #pragma unroll
-      for (int c = 0; c < 32; ++c) dst[c * RS] = (c == (int)kSeqEnd ? a.swar_restart : drop) | 0x10000u;
+      for (int c = 0; c < 32; ++c) dst[c * RS] = drop | 0x10000u;
     } else {
       const uint32_t q = a.qseq[(size_t)(t.q_first + slot) * a.L + (r - a.pad)];
       const uint4 *src = reinterpret_cast<const uint4 *>(s_enc + q * 32);
@@ -1397,14 +1398,18 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16(ScoreArgs a) {
 // of a row is then ONE v_pk_mad_u16 with op_sel instead of a v_perm_b32 that
 // pairs the two candidates' values plus a v_pk_mad_u16:
 //   lo = A.lo * B.hi + H.lo = vA * 1 + H.lo,   hi = A.hi * B.lo + H.hi = 1 * vB + H.hi
-// (per half modulo 2^16, as before). The END column's diagonal mask (m = 0 in
-// the END halves) becomes an AND of the previous column's H in those halves,
-// done in place before the rows, only on steps where some lane meets END. The
-// words take twice the LDS of the 16-bit rows, so a block holds the profiles
-// of at most kScoreQmaxUnit queries (the host uses this kernel when a segment
-// averages enough candidates per query to fill its blocks).
+// (per half modulo 2^16, as before). There is no m: the END column's rows come
+// out as RESTART through E instead of through a masked diagonal. The column
+// before an END floors E at RESTART in that half (the codes are loaded two
+// columns ahead), the END row of the profile is the drop (old H + drop stays far
+// below RESTART), so h = max3(s, E, F) = RESTART in every row; only a second
+// END in a window, whose older values reach above RESTART, resets E and the old
+// H explicitly (a wave-uniform branch). The words take twice the LDS of the
+// 16-bit rows, so a block holds the profiles of at most kScoreQmaxUnit queries
+// (the host uses this kernel when a segment averages enough candidates per
+// query to fill its blocks).
 template <int S, bool SWAR = false, bool UNIT = false>
-__global__ __launch_bounds__(kScoreBlock, 4) void k_score16f(ScoreArgs a) {  // 4 waves per SIMD: <= 128 VGPRs
+__global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
   static_assert(!UNIT || SWAR, "unit-pair words carry integer patterns");
   using C = Cells<true>;
   extern __shared__ __attribute__((aligned(16))) short s_prof16[];
@@ -1466,6 +1471,7 @@ __global__ __launch_bounds__(kScoreBlock, 4) void k_score16f(ScoreArgs a) {  // 
   const uint32_t NEXT32 = (uint32_t)(a.ext * 65537);
   const uint32_t ONE = SWAR ? 0x00010001u : C::kOne;
   const uint32_t RESTART = a.swar_restart * 0x10001u;
+  const uint32_t SWLOW = a.swar_low * 0x10001u;
 
   // Frame bases: until the window's first true END the frame is based near
   // -2040 (sigma(j) = -2040 + (G + j) * ext_pen), so every value there is
@@ -1498,6 +1504,15 @@ __global__ __launch_bounds__(kScoreBlock, 4) void k_score16f(ScoreArgs a) {  // 
   uint32_t c0A = dbp[xA], c0B = dbp[xB], c1A = dbp[xA + 1], c1B = dbp[xB + 1];
   const uint32_t steps = a.base + a.G - 1;
   const uint32_t wA_ = vA ? wA : 0u, wB_ = vB ? wB : 0u;
+  if constexpr (UNIT) {
+    // lane 0 starts at column 0 (no fill column sets E's floor for it): E enters
+    // as RESTART where that column is END, as after any column before an END
+    if (i == 0) {
+      const uint32_t e0 = PkSign(PkAddU16(c0A | (c0B << 16), 0x7FE77FE7u));
+#pragma unroll
+      for (int k = 0; k < S; ++k) E[k] = BfiV(e0, RESTART, E[k]);
+    }
+  }
   auto column = [&](uint32_t step, auto tested_c, auto fill_c) {
     constexpr bool tested = decltype(tested_c)::value, in_fill = decltype(fill_c)::value;
     uint32_t hin = ShiftUp(hout), fin = ShiftUp(fout);
@@ -1551,17 +1566,20 @@ __global__ __launch_bounds__(kScoreBlock, 4) void k_score16f(ScoreArgs a) {  // 
         const uint32_t reset = end & seen;
         seen |= end;
         if (__builtin_amdgcn_ballot_w64(reset != 0)) {  // wave-uniform: a real branch
+          if constexpr (UNIT) {
+            // a second END: values after the first one reach above RESTART, so
+            // E restarts explicitly and the old H (the diagonal inputs) drops
+            // to the frame base, where old H + drop stays far below RESTART
 #pragma unroll
-          for (int k = 0; k < S; ++k) E[k] = BfiV(reset, 0u, E[k]);
-        }
-        if constexpr (UNIT) {
-          // the diagonal mask: the previous column's H reads as 0 in the END
-          // halves (only the diagonal sums read the old H before the rows
-          // overwrite it; the row above's hand-over through hprev likewise)
-          const uint32_t keep = ~end;
+            for (int k = 0; k < S; ++k) {
+              E[k] = BfiV(reset, RESTART, E[k]);
+              H[k] = BfiV(reset, SWLOW, H[k]);
+            }
+            hprev = BfiV(reset, SWLOW, hprev);
+          } else {
 #pragma unroll
-          for (int k = 0; k < S; ++k) H[k] &= keep;
-          hprev &= keep;
+            for (int k = 0; k < S; ++k) E[k] = BfiV(reset, 0u, E[k]);
+          }
         }
       }
     }
@@ -1571,7 +1589,21 @@ __global__ __launch_bounds__(kScoreBlock, 4) void k_score16f(ScoreArgs a) {  // 
     const hf2 m = HF(mreg);
     // the next column's frame: one step on, or (f16) restarted at 0 after a true END
     const uint32_t zn = SWAR ? sigc + EXTP : BfiV(end, EXTP, W(HF(sig) + HF(EXTP)));
-    const hf2 Z1 = HF(zn);
+    uint32_t zf = zn;  // E's floor: real 0 of the next column's frame
+    if constexpr (UNIT) {
+      // UNIT: where the NEXT column is END, E's floor is RESTART, so every row
+      // of the END column enters with E = RESTART; its diagonal reads the
+      // profile's drop (old H + drop < RESTART) and F stays below, so each row
+      // comes out as RESTART = real 0 of the restarted frame without masking
+      // the old H. c0A/c0B hold the next column's codes (the END padding past a
+      // window cut at the DB's end; the drain columns' values are never read).
+      if (__builtin_amdgcn_ballot_w64(max((uint16_t)c0A, (uint16_t)c0B) >= (uint16_t)kSeqEnd)) {
+        uint32_t ne = PkSign(PkAddU16(c0A | (c0B << 16), 0x7FE77FE7u));
+        if constexpr (in_fill) ne = (int)(step - i) + 1 < 0 ? 0u : ne;  // the next column is still a fill column
+        zf = BfiV(ne, RESTART, zn);
+      }
+    }
+    const hf2 Z1 = HF(zf);
     lds_u4 *pA = (lds_u4 *)(uintptr_t)MadU24s(rA, RS2, baseA2);
     lds_u4 *pB = (lds_u4 *)(uintptr_t)MadU24s(rB, RS2, baseB2);
     uint32_t diag = diag0, F = fin, cm = sigc;
@@ -1579,33 +1611,14 @@ __global__ __launch_bounds__(kScoreBlock, 4) void k_score16f(ScoreArgs a) {  // 
       if constexpr (SWAR) return W(U2(h) * U2(mreg) + U2(p));  // v_pk_mad_u16
       else return C::Diag(h, m, p);
     };
-    // UNIT: the words of rows k..k+3 / k+4..k+7 (the next chunk's are loaded
-    // into them as soon as the current chunk's diagonal sums have read them)
-#ifndef GHOSTM_K2_PREFETCH
-#define GHOSTM_K2_PREFETCH 1
-#endif
-    constexpr bool PF = UNIT && GHOSTM_K2_PREFETCH;
-    u32x4 ua0{}, ua1{}, ub0{}, ub1{};
-    if constexpr (UNIT) {
-      ua0 = pA[0];
-      ub0 = pB[0];
-      ua1 = pA[1];
-      ub1 = pB[1];
-    }
 #pragma unroll
     for (int k = 0; k < S; k += 8) {
       uint32_t wa[8], wb[8];  // UNIT: one word per row; else two rows per word
       if constexpr (UNIT) {
-        if constexpr (!PF) {
-          if (k > 0) {
-            ua0 = pA[k / 4];
-            ub0 = pB[k / 4];
-            ua1 = pA[k / 4 + 1];
-            ub1 = pB[k / 4 + 1];
-          }
-        }
-        const u32x4 qa0 = ua0, qa1 = ua1;
-        const u32x4 qb0 = ub0, qb1 = ub1;
+        // (loading the next chunk's words as soon as these rows have read them
+        // measured no faster and needs 134 VGPRs)
+        const u32x4 qa0 = pA[k / 4], qa1 = pA[k / 4 + 1];
+        const u32x4 qb0 = pB[k / 4], qb1 = pB[k / 4 + 1];
         wa[0] = qa0.x; wa[1] = qa0.y; wa[2] = qa0.z; wa[3] = qa0.w;
         wa[4] = qa1.x; wa[5] = qa1.y; wa[6] = qa1.z; wa[7] = qa1.w;
         wb[0] = qb0.x; wb[1] = qb0.y; wb[2] = qb0.z; wb[3] = qb0.w;
@@ -1641,16 +1654,6 @@ __global__ __launch_bounds__(kScoreBlock, 4) void k_score16f(ScoreArgs a) {  // 
         H[k + u] = W(h);
         const hf2 oE = SWAR ? HF(W(h) + KOE32) : h + KOE;
         if (u + 2 < 8) s[u + 2] = dsum(H[k + u + 1], u + 2, p2);
-        if constexpr (PF) {
-          if (u == 1 && k + 8 < S) {  // rows k..k+3 read: the next chunk's first four
-            ua0 = pA[k / 4 + 2];
-            ub0 = pB[k / 4 + 2];
-          }
-          if (u == 5 && k + 8 < S) {  // rows k+4..k+7 read
-            ua1 = pA[k / 4 + 3];
-            ub1 = pB[k / 4 + 3];
-          }
-        }
         const hf2 G = __builtin_elementwise_maximum(HF(F), oE);
         E[k + u] = W(__builtin_elementwise_maximum(__builtin_elementwise_maximum(HF(E[k + u]), oE), Z1));
         F = SWAR ? W(G) + NEXT32 : W(G + NEXT);
