@@ -49,7 +49,8 @@ TB_OPS_PER_CELL = 20     # traceback cell with match/length bookk
 FULL_GOLDEN = os.path.join(REPO, "tests", "golden", "full_golden.json")
 VALU_ISSUE = os.path.join(REPO, "profiles", "r2_valu_issue.json")
 PMC = os.path.join(REPO, "profiles", "pmc_traffic.json")
-ISA_MIX = os.path.join(REPO, "profiles", "r3_k2_isa_mix.json")
+ISA_MIX = os.path.join(REPO, "profiles", "r3_k2_isa_mix.json")  # k_score16f<32, true> (16-bit profile rows)
+ISA_MIX_UNIT = os.path.join(REPO, "profiles", "r3u_k2_isa_mix.json")  # k_score16f<32, true, true> (unit-pair words)
 VOP2_IN_MIX_CYCLES = 3.44  # fast VOP2 add inside a 1:2 pk_max3:add stream (profiles/r2c_valu_issue_pmc.txt)
 
 
@@ -449,7 +450,12 @@ def main() -> None:
         peak = PEAK_VALU_PK16_TOPS if packed else PEAK_VALU_TOPS
         framed = half and per.get("score_launches_framed", 0) == per["score_launches"]
         swar = framed and per.get("score_launches_swar", 0) == per["score_launches"]
-        if swar:
+        unit = swar and per.get("score_launches_unit", 0) == per["score_launches"]
+        if unit:
+            kname = ("k_score16f<32,swar,unit> (K2 Gotoh DP, per-column frame over 16-bit integer patterns, "
+                     "two candidates per lane; unit-pair profile words: the diagonal sum is one op_sel "
+                     "v_pk_mad_u16)")
+        elif swar:
             kname = ("k_score16f<32,swar> (K2 Gotoh DP, per-column frame over 16-bit integer patterns: packed "
                      "f16 max3 on the patterns, v_add_u32 for the constant adds, two candidates per lane)")
         elif framed:
@@ -492,7 +498,7 @@ def main() -> None:
             # VOP2 2.27 alone and 3.44 at best inside VOP3P streams (the 1:2 mix
             # row). The ceiling takes the cheapest cost of each class, so the
             # kernel's PMC cycles per instruction cannot beat it.
-            mix = (_json(ISA_MIX) or {}).get("column_bodies")
+            mix = (_json(ISA_MIX_UNIT if unit else ISA_MIX) or {}).get("column_bodies")
             cyc = pmc.get("k_score_valu_cycles_per_inst")
             c3 = issue.get("cycles_per_inst", {}).get("vop3_class_median")
             if mix and cyc and c3:

@@ -2,7 +2,7 @@
 object of build/native/device.o (llvm-objdump). Used to price K2's issue
 ceiling by instruction class (bench.py `roofline.issue_ceiling`).
 
-    python tools/isa_mix.py [--kernel k_score16fILi32ELb1E] [--json out.json]
+    python tools/isa_mix.py [--kernel k_score16fILi32ELb1ELb1E] [--json out.json]
 
 Classes (measured in profiles/r2_valu_issue.json, tools/microbench/valu_issue.hip):
   fast VOP2  the e32 forms of add/sub/subrev/mul/fmac (f32/f16/u16/u32),
@@ -117,7 +117,7 @@ def mix(seg) -> dict:
 
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--kernel", default="k_score16fILi32ELb1E")
+    ap.add_argument("--kernel", default="k_score16fILi32ELb1ELb1E")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     body = kernel_body(disassemble(), a.kernel)
