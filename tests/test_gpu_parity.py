@@ -43,6 +43,22 @@ def test_gpu_matches_reference_golden(ds, var, opts, env, dataset, golden, tmp_p
     assert cases.sha256(str(tmp_path / "g.out")) == want["sha256"]
 
 
+@pytest.mark.parametrize("ds,var,opts,env", cases.VARIANTS, ids=[f"{v[0]}/{v[1]}" for v in cases.VARIANTS])
+def test_gpu_unit_k2_matches_reference_golden(ds, var, opts, env, dataset, golden, tmp_path):
+    """Every golden variant with K2's unit-pair kernel forced (GHOSTM_K2=unit;
+    by default it runs only on segments averaging >= 80 candidates per query):
+    windows crossing one or several subject ENDs (the testset's short
+    subjects), a window whose first column is END, the DB's end, one-subject
+    DBs, short queries (S = 16 and 8) and every gap setting."""
+    d = dataset(ds)
+    text, st = _gpu_text(d, opts, dict(env, GHOSTM_K2="unit"), str(tmp_path / "g.out"))
+    want = golden["aln"][f"{ds}/{var}"]
+    (tmp_path / "g.out").write_bytes(text)
+    assert cases.sha256(str(tmp_path / "g.out")) == want["sha256"]
+    if st["score_launches_swar"] == st["score_launches"] > 0:  # integer patterns fit: the unit kernel ran
+        assert st["score_launches_unit"] == st["score_launches"]
+
+
 @pytest.mark.parametrize("merge", ["device", "device_thread", "host"])
 @pytest.mark.parametrize("ds,var,opts,env", cases.BATCH_VARIANTS,
                          ids=[f"{v[0]}/{v[1]}" for v in cases.BATCH_VARIANTS])
