@@ -644,22 +644,56 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   __syncthreads();
   const uint32_t n = s_off[nl];
 
+  // 0. the list of every entry, one byte each, in the queue's LDS (dead until
+  //    pass 2): thread t finds the list of entry 16 t once (the chunk's first
+  //    list, then the boundaries up to it) and walks its 16 entries, so pass 1
+  //    reads an entry's list with one ds_read_u8 instead of a search per entry
+  static_assert(QCAP * 4 >= 16 * BLOCK && 16 * BLOCK >= 64 * KE * kW, "entry list bytes alias the queue");
+  uint8_t *const s_lst = reinterpret_cast<uint8_t *>(s_q);
+  {
+    const uint32_t e0 = tid * 16;
+    uint32_t wv[4] = {0, 0, 0, 0};  // entries past n: list 0 (read, never used)
+    if (e0 < n) {
+      uint32_t j = s_cfirst[e0 >> 6];
+      while (s_off[j + 1] <= e0) ++j;
+      uint32_t nxt = s_off[j + 1];
+#pragma unroll
+      for (uint32_t k = 0; k < 16; ++k) {
+        while (e0 + k >= nxt && j + 1 < nl) nxt = s_off[++j + 1];  // (empty lists: several steps)
+        wv[k >> 2] |= j << (8 * (k & 3));
+      }
+    }
+    reinterpret_cast<uint4 *>(s_lst)[tid] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+  }
+  __syncthreads();
+
   // 1. gather: chunk c = wave + kW * e (64 entries of the concatenated lists),
   //    lane = entry within the chunk; bins stay in registers
   uint32_t bin[KE];
 #pragma unroll
   for (uint32_t e0 = 0; e0 < KE; e0 += 4) {
-    uint32_t pos[4], prv[4], lst[4];
+    uint32_t pos[4], prv[4], lst[4], ii[4], jj[4], dd[4];
+    // the four entries' list bytes, then their position offsets, as two batches
+    // of LDS reads (every entry index stays inside the byte table)
 #pragma unroll
     for (uint32_t u = 0; u < 4; ++u) {
-      const uint32_t c = wave + kW * (e0 + u), i = (c << 6) + lane;
+      ii[u] = ((wave + kW * (e0 + u)) << 6) + lane;
+      jj[u] = s_lst[ii[u]];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) dd[u] = s_delta[jj[u]];
+    // (kept here: the compiler otherwise sinks both reads into each entry's
+    // branch below and waits for them one entry at a time)
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) asm volatile("" : "+v"(dd[u]));
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) {
+      const uint32_t i = ii[u], j = jj[u];
       pos[u] = 0;
       prv[u] = kNone;
       lst[u] = kNone;
       if (i < n) {
-        uint32_t j = s_cfirst[c];
-        while (s_off[j + 1] <= i) ++j;
-        const uint32_t at = i + s_delta[j];  // = list_beg[j] + (i - s_off[j])
+        const uint32_t at = i + dd[u];  // = list_beg[j] + (i - s_off[j])
         pos[u] = a.positions[at];
         lst[u] = j;
         if (lane == 0 && i != s_off[j]) prv[u] = a.positions[at - 1];
