@@ -79,6 +79,7 @@ struct DeviceTimes {
   uint64_t seed_queries_wide = 0;                 // ... redone by the offset pass (more than a slot)
   uint64_t seed_launches_filter = 0;              // Seed() calls whose classes 0/1 ran k_seed_filter
   uint64_t traceback_launches_scan_swar = 0;  // K3a scans over 16-bit integer patterns
+  uint64_t traceback_launches_strips = 0;  // key DPs run by strip class (lanes of strips 0..i* only)
   uint64_t score_launches_swar = 0;  // ... of the framed kernel over 16-bit integer patterns (k_score16f<S, true>)
   uint64_t score_launches_unit = 0;  // ... of its unit-pair profile variant (k_score16f<S, true, true>)
   uint64_t seed_filter_overflows = 0;             // ... queries redone by k_seed_hash (queue overflow)

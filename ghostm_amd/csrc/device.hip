@@ -142,7 +142,7 @@ struct DeviceModule::Impl {
   } score_state;
   // K3 work (tb_sort: two histograms + total, two cursor arrays)
   DevBuf tb_qid, tb_end, tb_start, tb_ml;
-  DevBuf tb_width, tb_ncols, tb_key, tb_order1, tb_order2, tb_sort, tb_pair_a, tb_pair_b, tb_best;
+  DevBuf tb_width, tb_ncols, tb_skey, tb_key, tb_order1, tb_order2, tb_sort, tb_pair_a, tb_pair_b, tb_best;
   int cus = 256;
   // K4 work
   DevBuf keys, sel_count, sel_score, sel_sid, slot_hits, sel_from;
@@ -1153,16 +1153,23 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
     I.tb_pair_a.Reserve((size_t)n * 4);
     I.tb_pair_b.Reserve((size_t)n * 4);
     I.tb_best.Reserve((size_t)n * 4);
-    I.tb_sort.Reserve((size_t)(4 * NB + 2) * 4);
+    I.tb_skey.Reserve((size_t)n * 4);
+    // two histograms + totals, two cursor arrays, the key DP's strip-class offsets
+    constexpr uint32_t kClassWords = kern::kTbStripClasses + 1;
+    I.tb_sort.Reserve((size_t)(4 * NB + 2 + kClassWords) * 4);
     uint32_t *hist1 = I.tb_sort.as<uint32_t>(), *hist2 = hist1 + NB + 1;
-    uint32_t *cur1 = hist2 + NB + 1, *cur2 = cur1 + NB;
-    HIP_CHECK(hipMemsetAsync(I.tb_sort.p, 0, (size_t)(4 * NB + 2) * 4, S(stream_)));
+    uint32_t *cur1 = hist2 + NB + 1, *cur2 = cur1 + NB, *class_off = cur2 + NB;
+    HIP_CHECK(hipMemsetAsync(I.tb_sort.p, 0, (size_t)(4 * NB + 2 + kClassWords) * 4, S(stream_)));
+    // strip classes for the key DP when a group has at most kTbStripClasses
+    // lanes (GHOSTM_K3_STRIPS=0 keeps every hit on all of them)
+    const char *strips_env = getenv("GHOSTM_K3_STRIPS");
+    const bool strips = lay.G <= kern::kTbStripClasses && !(strips_env && strcmp(strips_env, "0") == 0);
     const dim3 g256((n + 255) / 256), b256(256);
     const uint32_t *subj = d && d->nsubj ? d->subj.as<uint32_t>() : nullptr;
     hipLaunchKernelGGL(kern::k_tb_prep, g256, b256, 0, S(stream_), a.qid, a.end, n, a.base, subj,
                        subj ? d->nsubj : 0u, subj ? d->subj_bucket.as<uint32_t>() : nullptr, d ? d->len : 0u,
                        I.tb_width.as<uint32_t>(),
-                       I.tb_ncols.as<uint32_t>(), hist2);  // empty slots -> hist2[0]
+                       I.tb_ncols.as<uint32_t>(), I.tb_skey.as<uint32_t>(), hist2);  // empty slots -> hist2[0]
     const uint32_t ps = std::max<uint32_t>(pair_span, 1);
     const uint32_t runs_per_span = (ps + kern::kPairRun - 1) / kern::kPairRun;
     const uint64_t runs = (uint64_t)((n + ps - 1) / ps) * runs_per_span;
@@ -1212,6 +1219,8 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
     const bool exact = subj != nullptr;
     sa.best_out = I.tb_best.as<uint32_t>();
     sa.swar_low = (uint32_t)swar_low;
+    sa.skey = I.tb_skey.as<uint32_t>();
+    sa.strips = strips ? 1u : 0u;
 #define GHOSTM_SCAN1(SS, HH, EE, FF)                                                                          \
   hipLaunchKernelGGL((kern::k_tb_scan<SS, HH, EE, FF>), dim3(blocks), dim3(kern::kScanBlock), kScanLds, S(stream_), \
                      sa)
@@ -1235,8 +1244,10 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
 #undef GHOSTM_SCAN
 #undef GHOSTM_SCANW
 #undef GHOSTM_SCAN1
-    hipLaunchKernelGGL(kern::k_csort_scatter, gsort, b256, 0, S(stream_), I.tb_ncols.as<uint32_t>(), n, false,
-                       hist2, cur2, I.tb_order2.as<uint32_t>());
+    hipLaunchKernelGGL(kern::k_csort_scatter, gsort, b256, 0, S(stream_), I.tb_skey.as<uint32_t>(), n, false,
+                       hist2, cur2, I.tb_order2.as<uint32_t>(), strips ? class_off : nullptr);
+    a.class_off = strips ? class_off : nullptr;
+    times_.traceback_launches_strips += strips ? 1 : 0;
     HIP_CHECK(hipGetLastError());
     a.order = I.tb_order2.as<uint32_t>();
     a.ncols = I.tb_ncols.as<uint32_t>();
@@ -1246,7 +1257,9 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
     times_.traceback_launches_scan_swar += swar ? 1 : 0;
   }
   const uint32_t per_block = (kern::kTbBlock / 64) * lay.gpw;
-  const dim3 grid((n + per_block - 1) / per_block), block(kern::kTbBlock);
+  // strip classes: each class rounds its last wave up, so one more block covers
+  // the (at most kTbStripClasses) extra waves
+  const dim3 grid((n + per_block - 1) / per_block + (a.class_off ? 1 : 0)), block(kern::kTbBlock);
   const bool fin = a.best_h != nullptr;  // the scan's maxima: no running maximum in the key DP
 #define GHOSTM_TB(SS)                                                                                              \
   if (key16 && fin) hipLaunchKernelGGL((kern::k_traceback_key<SS, 16, true>), grid, block, 0, S(stream_), a);      \

@@ -1801,7 +1801,13 @@ struct TbArgs {
   // k_rev_codes' packed row offsets of every query (per query Lpad / 4 words),
   // when the scan made them; null = built from qseq bytes
   const uint32_t *rcodes;
+  // strip classes (FINAL key DP, G <= kTbStripClasses): order[] holds class c's
+  // hits at [class_off[c], class_off[c + 1]), each with its first maximal cell
+  // in strip c; a wave of class c runs groups of c + 1 lanes (rows 0..S(c+1)),
+  // 64 / (c + 1) hits per wave. null = every hit runs all G strips
+  const uint32_t *class_off;
 };
+constexpr uint32_t kTbStripClasses = 4;
 
 // the wave's largest value (loop bound of a lane-group loop)
 __device__ inline uint32_t WaveMax(uint32_t v) {
@@ -1958,9 +1964,28 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
   __syncthreads();
 
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t g = lane / a.G, i = lane - g * a.G;
-  const uint32_t idx = (blockIdx.x * (kTbBlock / 64) + wave) * a.gpw + g;
-  const bool in_range = g < a.gpw && idx < a.n;
+  // strip classes (FINAL, class_off): the waves of class c come after those of
+  // classes < c, each running 64 / (c + 1) hits in groups of c + 1 lanes
+  uint32_t G = a.G, gpw = a.gpw, wv = blockIdx.x * (kTbBlock / 64) + wave, lo = 0, hi = a.n;
+  if (FINAL && a.class_off) {
+    uint32_t c = 0;
+    for (; c < kTbStripClasses; ++c) {
+      const uint32_t clo = a.class_off[c], chi = a.class_off[c + 1];
+      const uint32_t gp = 64 / (c + 1), waves = (chi - clo + gp - 1) / gp;
+      if (wv < waves) {
+        G = c + 1;
+        gpw = gp;
+        lo = clo;
+        hi = chi;
+        break;
+      }
+      wv -= waves;
+    }
+    if (c == kTbStripClasses) return;  // past the last class's waves (no barrier below)
+  }
+  const uint32_t g = lane / G, i = lane - g * G;
+  const uint32_t idx = lo + wv * gpw + g;
+  const bool in_range = g < gpw && idx < hi;
   const uint32_t hit = in_range && a.order ? a.order[idx] : idx;
   const bool valid = in_range && a.qid[hit] != 0xFFFFFFFFu;
   uint32_t p0 = 0, width = 0;
@@ -2008,7 +2033,7 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
   const uint32_t HIGH = ~KL::kLow;
   int j = -(int)i;
   const uint32_t wmax = WaveMax(valid ? width : 0u);
-  const uint32_t steps = wmax ? wmax + a.G - 1 : 0u;
+  const uint32_t steps = wmax ? wmax + G - 1 : 0u;
   for (uint32_t step = 0; step < steps; ++step, ++j) {
     int kin = ShiftUpI(kout), kfin = ShiftUpI(kfout);
     if (i == 0) { kin = 0; kfin = 0; }
@@ -2082,8 +2107,8 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
       for (int u = S - 1; u >= 0; --u)
         if (((uint32_t)K[u] >> KL::kHS) == bh) { found = 1; fml = (int)((uint32_t)K[u] & KL::kMl); }
     }
-    for (uint32_t k = 1; k < a.G; ++k) {
-      const int src = (int)(g * a.G + k);
+    for (uint32_t k = 1; k < G; ++k) {
+      const int src = (int)(g * G + k);
       const int of = __shfl(found, src), om = __shfl(fml, src);
       if (!found && of) { found = 1; fml = om; }
     }
@@ -2094,8 +2119,8 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
     int B = bestK >> KL::kHS;
     C = best_col;
     ML = (int)((uint32_t)bestK & KL::kMl);
-    for (uint32_t k = 1; k < a.G; ++k) {
-      const int src = (int)(g * a.G + k);
+    for (uint32_t k = 1; k < G; ++k) {
+      const int src = (int)(g * G + k);
       const int ok = __shfl(bestK, src), oc = __shfl(best_col, src);
       const int ob = ok >> KL::kHS;
       if (ob > B || (ob == B && ob > 0 && oc < C)) { B = ob; C = oc; ML = (int)((uint32_t)ok & KL::kMl); }
@@ -2555,6 +2580,7 @@ __global__ void k_records(const uint32_t *sel_count, const SlotHit *slots, const
 // k_tb_scan and the hits by j* + 1 for the key kernel, so each wave's lane
 // groups run windows of about the same length.
 constexpr uint32_t kSortBins = 1024;   // counting-sort keys (column counts), clamped
+constexpr uint32_t kStripBins = 256;   // ... per strip class of the key DP (kTbStripClasses classes)
 // one workgroup per CU (the pair table fills the LDS) of 12 waves: 3 per SIMD
 // leave 168 VGPRs, room for an 8-row read-ahead (1024 threads, 128 VGPRs and a
 // 4-row read-ahead measured 56.5 against 55.8 ms of K3 per step, same box)
@@ -2572,7 +2598,7 @@ constexpr uint32_t kPairWords = kPairCodes * kPairCodes * kPairStride;
 __global__ __launch_bounds__(256) void k_tb_prep(const uint32_t *qid, const uint32_t *end, uint32_t n,
                                                  uint32_t base, const uint32_t *subj, uint32_t nsubj,
                                                  const uint32_t *subj_bucket, uint32_t dblen, uint32_t *width,
-                                                 uint32_t *ncols, uint32_t *empty) {
+                                                 uint32_t *ncols, uint32_t *skey, uint32_t *empty) {
   __shared__ uint32_t s_empty;
   if (threadIdx.x == 0) s_empty = 0;
   __syncthreads();
@@ -2589,6 +2615,7 @@ __global__ __launch_bounds__(256) void k_tb_prep(const uint32_t *qid, const uint
     }
     width[k] = w;
     ncols[k] = 0;
+    skey[k] = 0;
     if (!w) atomicAdd(&s_empty, 1u);
   }
   __syncthreads();
@@ -2665,7 +2692,7 @@ constexpr uint32_t kCsortItems = 16;
 constexpr uint32_t kCsortTile = 256 * kCsortItems;
 __global__ __launch_bounds__(256) void k_csort_scatter(const uint32_t *key, uint32_t n, bool skip_zero,
                                                        const uint32_t *hist, uint32_t *cursor,
-                                                       uint32_t *order) {
+                                                       uint32_t *order, uint32_t *class_off = nullptr) {
   static_assert(kSortBins == 4 * 256 && kSortBins == 1024, "four bins per thread, ten key bits");
   __shared__ uint32_t s_pre[kSortBins];
   __shared__ uint32_t s_cnt[kSortBins];
@@ -2694,6 +2721,9 @@ __global__ __launch_bounds__(256) void k_csort_scatter(const uint32_t *key, uint
     s_pre[t * 4 + u] = run;
     run += v[u];
   }
+  // the first position of every kStripBins-wide key class, and the total
+  if (class_off && blockIdx.x == 0 && t % (kStripBins / 4) == 0) class_off[t / (kStripBins / 4)] = s_pre[t * 4];
+  if (class_off && blockIdx.x == 0 && t == 255) class_off[kSortBins / kStripBins] = run;
   __syncthreads();
   const unsigned long long lt = (1ull << lane) - 1;
   const uint32_t first = blockIdx.x * kCsortTile + t;
@@ -2740,9 +2770,14 @@ struct TbScanArgs {
   int open, ext;
   uint32_t *ncols;             // per slot: j* + 1
   uint32_t *best_out;          // per slot: the reverse DP's maximum
-  uint32_t *hist;              // histogram of ncols (kSortBins)
+  uint32_t *hist;              // histogram of skey (kSortBins)
   unsigned long long *cells;   // += L x scanned columns
   uint32_t swar_low;           // SWAR: the frame base (integer patterns, as K2's)
+  // per slot: the key DP's sort key. strips (G <= 4): (first strip holding the
+  // maximal cell) * kStripBins + min(j* + 1, kStripBins - 1), so the key DP
+  // runs the lanes of strips 0..i* only (kTbStripClasses); else min(j* + 1, kSortBins - 1)
+  uint32_t *skey;
+  uint32_t strips;
 };
 
 // Per query, the table byte offsets (code * 4) of its rows in the reverse DP's
@@ -3018,22 +3053,33 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
     }
     int BA = SWAR ? (int)(best & 0xFFFFu) : C::Decode(best & 0xFFFFu), CA = (int)(col & 0xFFFFu);
     int BB = SWAR ? (int)(best >> 16) : C::Decode(best >> 16), CB = (int)(col >> 16);
-    // first column over the group's row strips
+    // first column over the group's row strips, and the first strip (lane)
+    // holding a maximal cell there: the first maximal cell in processing order
+    // lies in strip IA, and no cell of a later strip feeds it
+    uint32_t IA = 0, IB = 0;
     for (uint32_t k = 1; k < a.G; ++k) {
       const int src = (int)(g * a.G + k);
       const int oba = __shfl(BA, src), oca = __shfl(CA, src);
       const int obb = __shfl(BB, src), ocb = __shfl(CB, src);
-      if (oba > BA || (oba == BA && oca < CA)) { BA = oba; CA = oca; }
-      if (obb > BB || (obb == BB && ocb < CB)) { BB = obb; CB = ocb; }
+      if (oba > BA || (oba == BA && oca < CA)) { BA = oba; CA = oca; IA = k; }
+      if (obb > BB || (obb == BB && ocb < CB)) { BB = obb; CB = ocb; IB = k; }
     }
+    auto skey = [&](int c, uint32_t strip, int b) -> uint32_t {
+      if (!a.strips) return min((uint32_t)c + 1, kSortBins - 1);
+      return (b > 0 ? strip : 0u) * kStripBins + min((uint32_t)c + 1, kStripBins - 1);
+    };
     if (i == 0 && wA) {
       a.ncols[sA] = (uint32_t)CA + 1;
       a.best_out[sA] = (uint32_t)BA;
-      atomicAdd(&s_hist[min((uint32_t)CA + 1, kSortBins - 1)], 1u);
+      const uint32_t kA = skey(CA, IA, BA);
+      a.skey[sA] = kA;
+      atomicAdd(&s_hist[kA], 1u);
       if (wB) {
         a.ncols[sB] = (uint32_t)CB + 1;
         a.best_out[sB] = (uint32_t)BB;
-        atomicAdd(&s_hist[min((uint32_t)CB + 1, kSortBins - 1)], 1u);
+        const uint32_t kB = skey(CB, IB, BB);
+        a.skey[sB] = kB;
+        atomicAdd(&s_hist[kB], 1u);
       }
     }
     WaveAddCells(a.cells, i == 0 ? (unsigned long long)(wA + wB) * a.L : 0ull);

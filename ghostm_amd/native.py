@@ -78,6 +78,7 @@ class GhostmStats(ctypes.Structure):
         ("traceback_launches_scan_swar", c_uint64),
         ("seed_list_entries", c_uint64),
         ("score_launches_unit", c_uint64),
+        ("traceback_launches_strips", c_uint64),
     ]
 
     def as_dict(self) -> dict:

@@ -203,6 +203,7 @@ typedef struct GhostmStats {
   uint64_t traceback_launches_scan_swar; /* K3a scans over 16-bit integer patterns (k_tb_scan<..., true>) */
   uint64_t seed_list_entries;       /* K1: sum over queries of the k-mer position-list lengths */
   uint64_t score_launches_unit;     /* framed integer-pattern K2 launches with unit-pair profile words (k_score16f<S, true, true>) */
+  uint64_t traceback_launches_strips; /* K3 key DPs run by strip class (each hit on the strips up to its first maximal cell) */
 } GhostmStats;
 
 /* Session: parse `aln` options exactly like the reference (getopt string

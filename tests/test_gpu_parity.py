@@ -223,7 +223,7 @@ def test_reference_gpu_batching_rule(dataset):
 
 
 @pytest.mark.parametrize("kind", ["int32", "int16", "f16plain", "f16frame", "swar16", "unit", "k2_nowait", "k3_int32",
-                                  "k1_merge"])
+                                  "k3_nostrips", "k1_merge"])
 @pytest.mark.parametrize("ds,var,opts", [("syn_small", "default", []), ("syn_short", "default", []),
                                          ("syn_small", "r64_pam250", ["-r", "64", "-M", cases.PAM250, "-y", "2"])])
 def test_forced_score_encoding_matches_golden(kind, ds, var, opts, dataset, golden, tmp_path):
@@ -232,6 +232,7 @@ def test_forced_score_encoding_matches_golden(kind, ds, var, opts, dataset, gold
     scores may exceed int16. Forced with GHOSTM_K2 each reproduces the golden."""
     d = dataset(ds)
     env = ({"GHOSTM_K3": "int32"} if kind == "k3_int32" else
+           {"GHOSTM_K3_STRIPS": "0"} if kind == "k3_nostrips" else
            {"GHOSTM_K1": "merge"} if kind == "k1_merge" else
            {"GHOSTM_K2_NOWAIT": "1"} if kind == "k2_nowait" else {"GHOSTM_K2": kind})
     text, st = _gpu_text(d, opts, env, str(tmp_path / "g.out"))
@@ -240,6 +241,8 @@ def test_forced_score_encoding_matches_golden(kind, ds, var, opts, dataset, gold
     assert st["traceback_launches"] > 0
     if kind == "k3_int32":
         assert st["traceback_launches_key"] == 0
+    elif kind == "k3_nostrips":  # every hit's key DP on all of its group's strips
+        assert st["traceback_launches_strips"] == 0 and st["traceback_launches_key"] > 0
     elif kind == "k1_merge":
         assert st["seed_runs_hash"] == 0
     elif kind == "k2_nowait":  # K2 launches without a host wait, timings resolved at the end
@@ -264,6 +267,7 @@ def test_default_encoding_is_f16_when_scores_fit(dataset, golden, tmp_path):
     assert st["score_launches_framed"] == st["score_launches"]  # k_score16f, the column-framed kernel
     assert st["score_launches_swar"] == st["score_launches"]  # ... over 16-bit integer patterns
     assert st["traceback_launches_key"] == st["traceback_launches"] > 0
+    assert st["traceback_launches_strips"] == st["traceback_launches"]  # key DP by strip class
     assert st["seed_runs_hash"] > 0
     # PAM250 at L = 127 can reach 2159 > 2047: f16 runs with the re-score guard
     text2, st2 = _gpu_text(d, ["-M", cases.PAM250, "-G", "8", "-E", "1", "-y", "2"], {},
