@@ -144,7 +144,8 @@ class Session:
 
     def stats(self) -> dict:
         st = native.GhostmStats()
-        native.load().GhostmSessionStats(self._h, ctypes.byref(st))
+        # the sized call: a library built with more fields writes only ours
+        native.load().GhostmSessionStatsSized(self._h, ctypes.byref(st), ctypes.sizeof(st))
         return st.as_dict()
 
     def close(self) -> None:

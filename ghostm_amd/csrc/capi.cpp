@@ -1,4 +1,5 @@
 // capi.cpp — session part of the C ABI (include/ghostm_hip.h Part 2).
+#include <algorithm>
 #include <cstring>
 #include <fstream>
 #include <iostream>
@@ -130,6 +131,13 @@ int GhostmSessionStats(void *s, GhostmStats *stats) {
   if (!s || !stats) return 1;
   *stats = static_cast<Session *>(s)->Stats();
   return 0;
+}
+
+size_t GhostmSessionStatsSized(void *s, GhostmStats *stats, size_t size) {
+  if (!s || !stats) return 0;
+  const GhostmStats &st = static_cast<Session *>(s)->Stats();
+  std::memcpy(stats, &st, std::min(size, sizeof(GhostmStats)));
+  return sizeof(GhostmStats);
 }
 
 void GhostmSessionDestroy(void *s) { delete static_cast<Session *>(s); }

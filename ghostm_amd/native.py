@@ -128,6 +128,7 @@ SIGNATURES = {
     "GhostmSessionHits": (c_size_t, [c_void_p, POINTER(GhostmHit), c_size_t]),
     "GhostmSessionDeviceHits": (c_size_t, [c_void_p, c_void_p, c_size_t]),
     "GhostmSessionStats": (c_int, [c_void_p, POINTER(GhostmStats)]),
+    "GhostmSessionStatsSized": (c_size_t, [c_void_p, POINTER(GhostmStats), c_size_t]),
     "GhostmSessionDestroy": (None, [c_void_p]),
     "GhostmAlignMain": (c_int, [c_int, POINTER(c_char_p)]),
 }

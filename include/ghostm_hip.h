@@ -291,6 +291,13 @@ size_t GhostmSessionDeviceHits(void *session, void *dst_device, size_t cap);
 
 int GhostmSessionStats(void *session, GhostmStats *stats);
 
+/* The same with the caller's struct size: GhostmStats only ever grows by
+ * fields appended at its end, so a caller built against an older header
+ * passes its sizeof and gets exactly the fields it knows (min(size, the
+ * library's sizeof) bytes are written). Returns the library's sizeof, or 0 on
+ * a null argument. */
+size_t GhostmSessionStatsSized(void *session, GhostmStats *stats, size_t size);
+
 void GhostmSessionDestroy(void *session);
 
 /* `ghostm aln ...` end to end (create + run + write + destroy). Exit status like

@@ -406,3 +406,20 @@ def test_gpu_ungapped_karlin_evalues(dataset, tmp_path):
         want = (np.float32(int(fb[2])) * lam - logk) / ln2
         assert float(fa[8]) == pytest.approx(float(want), rel=1e-5)  # %g keeps 6 digits
         assert float(fa[7]) >= 0.0  # underflows to 0 for long exact matches, as in float
+
+
+def test_stats_sized_writes_only_the_callers_fields(dataset, tmp_path):
+    """GhostmSessionStatsSized: a caller built against an older, shorter
+    GhostmStats gets exactly its prefix; the return value is the library's size."""
+    d = dataset("syn_small")
+    lib = native.load()
+    with Session(["-i", f"{d}/q", "-d", f"{d}/db", "-o", str(tmp_path / "x"), "-D", "0"]) as s:
+        s.run()
+        full = native.GhostmStats()
+        assert lib.GhostmSessionStatsSized(s._h, ctypes.byref(full), ctypes.sizeof(full)) == ctypes.sizeof(full)
+        buf = (ctypes.c_ubyte * ctypes.sizeof(full))()
+        assert lib.GhostmSessionStatsSized(s._h, ctypes.cast(buf, ctypes.POINTER(native.GhostmStats)), 64) \
+            == ctypes.sizeof(full)
+        raw = bytes(buf)
+        assert raw[:64] == bytes(full)[:64] and not any(raw[64:])
+        assert full.candidates > 0 and s.stats()["candidates"] == full.candidates
