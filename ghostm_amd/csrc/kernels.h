@@ -627,7 +627,11 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   if (q == kNoQuery) return;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t nl = a.nlists;
-  for (uint32_t k = tid; k < kFWords + TSLOTS; k += BLOCK) s_dyn[k] = 0;
+  // filter bitmap and exact table zeroed with 16-byte stores (both are
+  // multiples of four words, s_dyn 16-byte aligned)
+  static_assert(kFWords % 4 == 0 && TSLOTS % 4 == 0, "16-byte zeroing");
+  for (uint32_t k = tid; k < (kFWords + TSLOTS) / 4; k += BLOCK)
+    reinterpret_cast<uint4 *>(s_dyn)[k] = make_uint4(0u, 0u, 0u, 0u);
   if (tid == 0) s_qn = 0;
   uint32_t len = 0, beg = 0;
   if (tid < nl) {
