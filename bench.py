@@ -12,11 +12,17 @@ formatting (in memory) -> (N > 1) the one RCCL gather of the 32-byte hit records
 to rank 0.
 
 Multi-GPU (north_star: "shard the query batch across the 8 GPUs ... single RCCL
-gather"): one process per GPU (torchrun). ONE query set is cut into N balanced,
-name-group-aligned shards (GhostmSessionCreateShard); each rank searches its
-shard against a full DB replica, so total work is fixed as N grows ("strong").
-After the timed steps every rank writes its text at its offset of one output
-file, and rank 0 checks the assembled file against the reference pin.
+gather"): one process per GPU. `--gpus N` without WORLD_SIZE starts the N ranks
+itself (ghostm_amd/launch.py: children spawned before any GPU call, rank 0's
+line forwarded); under torchrun WORLD_SIZE must equal --gpus. ONE query set is
+cut into N balanced, name-group-aligned shards (GhostmSessionCreateShardEx);
+each rank searches its shard against a full DB replica, so total work is fixed
+as N grows ("strong"). Each rank is pinned to its GPU's NUMA-local CPUs. A step
+ends with one MIN all-reduce of every rank's ok flag (one rank's failure stops
+all ranks) and the one data-path collective: a gather of fixed-capacity hit
+record buffers with a count header. After the timed steps every rank writes its
+text at its offset of one output file, and rank 0 checks the assembled file
+against the reference pin.
 
 Parity in the line: `full_output_matches_reference` compares the sha256 of the
 whole output of the last timed step (N = 1) or of the assembled file (N > 1) with
@@ -27,6 +33,7 @@ the reference CPU program's output for the same full workload
 from __future__ import annotations
 
 import argparse
+import datetime
 import hashlib
 import json
 import os
@@ -39,7 +46,7 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-from ghostm_amd import workloads  # noqa: E402
+from ghostm_amd import launch, workloads  # noqa: E402
 
 PEAK_VALU_TOPS = 78.6   # 256 CU x 4 SIMD x 32 lanes/cycle x 2.4 GHz int32 ops (MI355X_MICROARCH.md)
 PEAK_VALU_PK16_TOPS = 157.3  # the same issue rate, two 16-bit ops per lane (v_pk_*)
@@ -48,7 +55,7 @@ SCORE_OPS_PER_CELL = 10  # Gotoh cell: add, max3 (H), add (open), add+max (E), a
 TB_OPS_PER_CELL = 20     # traceback cell with match/length bookkeeping
 FULL_GOLDEN = os.path.join(REPO, "tests", "golden", "full_golden.json")
 VALU_ISSUE = os.path.join(REPO, "profiles", "r2_valu_issue.json")
-PMC = os.path.join(REPO, "profiles", "pmc_traffic.json")
+PMC = os.path.join(REPO, "profiles", "pmc_traffic.json")  # cfg4; other presets: pmc_traffic_<preset>.json
 ISA_MIX = os.path.join(REPO, "profiles", "r3_k2_isa_mix.json")  # k_score16f<32, true> (16-bit profile rows)
 ISA_MIX_UNIT = os.path.join(REPO, "profiles", "r3u_k2_isa_mix.json")  # k_score16f<32, true, true> (unit-pair words)
 VOP2_IN_MIX_CYCLES = 3.44  # fast VOP2 add inside a 1:2 pk_max3:add stream (profiles/r2c_valu_issue_pmc.txt)
@@ -216,9 +223,21 @@ def full_pin(preset: str, nq: int, aln: list) -> dict | None:
     return pin
 
 
+def max_hits_per_query(aln: list) -> int:
+    """-b (hits kept per query, reference default 10), as getopt reads it."""
+    best = 10
+    for i, a in enumerate(aln):
+        if a == "-b" and i + 1 < len(aln):
+            best = int(aln[i + 1])
+        elif a.startswith("-b") and len(a) > 2:
+            best = int(a[2:])
+    return best
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one process per GPU); without WORLD_SIZE, N > 1 starts them itself")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--preset", choices=sorted(workloads.WORKLOADS), default="cfg4",
@@ -233,14 +252,19 @@ def main() -> None:
     ap.add_argument("--workdir", default=None)
     ap.add_argument("--aln", default="", help="extra aln options appended to the preset's (e.g. '-l 16')")
     args = ap.parse_args()
+    # before anything touches the GPU: launch the ranks ourselves, or check
+    # that torchrun's world is the one asked for
+    world, spawn = launch.world_from_env(args.gpus)
+    if spawn:
+        sys.exit(launch.spawn([os.path.abspath(__file__)] + sys.argv[1:], world))
     preset = args.preset
     w = workloads.WORKLOADS[preset]
     nq = args.queries or w["queries"]
     aln_args = list(w["aln"]) + args.aln.split()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     dist = None
+    placement = None
     # GHOSTM_BENCH_DIST=1 takes the collective path at world 1 too (under
     # torchrun --nproc-per-node 1): RCCL init, the record gather, the reductions
     if world > 1 or os.environ.get("GHOSTM_BENCH_DIST") == "1":
@@ -251,11 +275,15 @@ def main() -> None:
         # RCCL ("nccl") over xGMI; GHOSTM_BENCH_BACKEND=gloo rehearses the same
         # calls on a one-GPU machine (RCCL refuses two ranks on one device)
         backend = os.environ.get("GHOSTM_BENCH_BACKEND", "nccl")
+        # a rank that never arrives ends the job instead of hanging it
+        timeout = datetime.timedelta(seconds=float(os.environ.get("GHOSTM_BENCH_PG_TIMEOUT", "900")))
         if backend == "nccl":
-            dist.init_process_group(backend, device_id=torch.device("cuda", _device()))
+            dist.init_process_group(backend, device_id=torch.device("cuda", _device()), timeout=timeout)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=timeout)
         coll_dev = "cuda" if backend == "nccl" else "cpu"
+        if os.environ.get("GHOSTM_BENCH_NO_BIND") != "1":
+            placement = launch.bind_numa(dist, rank, _device())
     from ghostm_amd.aligner import HIT_DTYPE, Session
 
     # one data set for the whole job, built by rank 0 (ranks share the host)
@@ -285,16 +313,44 @@ def main() -> None:
 
         return Session(argv, shard=(rank, world), exchange=torch_allgather(dist, device=coll_dev))
 
-    sess = open_session()
+    def guarded(fn, what):
+        """fn() on every rank, then one ok-flag all-reduce: any rank's failure
+        raises on every rank (its own error on the failing one)."""
+        if dist is None:
+            return fn()
+        try:
+            out = fn()
+        except BaseException:
+            launch.agree(dist, False, coll_dev, what)
+            raise
+        launch.agree(dist, True, coll_dev, what)
+        return out
+
+    sess = guarded(open_session, "session create")
+    gatherer = None
+    if dist is not None:
+        import torch
+
+        from ghostm_amd.shard import RecordGather
+
+        # fixed capacity: the most hits any shard can return (queries x -b)
+        b, e = sess.shard_range() if world > 1 else (0, nq)
+        cap = torch.tensor([(min(e, nq) - b) * max_hits_per_query(aln_args)], device=coll_dev, dtype=torch.int64)
+        dist.all_reduce(cap, op=dist.ReduceOp.MAX)
+        gatherer = RecordGather(dist, int(cap.item()), HIT_DTYPE.itemsize, coll_dev)
 
     def step():
-        sess.run()
-        if dist is not None:
-            from ghostm_amd.shard import gather_device_records
-
+        guarded(sess.run, "run")
+        if gatherer is not None:
+            if coll_dev == "cuda":
+                n = sess.device_hits_into(gatherer.payload(), gatherer.cap)
+            else:  # gloo rehearsal: the records still leave the GPU by a device copy
+                recs = sess.device_hits()
+                n = recs.numel() // HIT_DTYPE.itemsize
+                gatherer.payload()[: recs.numel()].copy_(recs)
+            gatherer.set_count(n)
             # the single data-path collective: hit records to rank 0
-            step.merged = gather_device_records(sess.device_hits().to(coll_dev), dist, HIT_DTYPE.itemsize)
-    step.merged = None
+            gatherer.gather()
 
     for _ in range(args.warmup):
         step()
@@ -330,7 +386,7 @@ def main() -> None:
         dist.all_reduce(res)
         total_res = float(res.item())
         # each rank's step breakdown, and the GPUs the ranks actually ran on
-        mine = {"rank": rank, "device": _device(), "host": os.uname().nodename,
+        mine = {"rank": rank, "device": _device(), "host": os.uname().nodename, "placement": placement,
                 "ms_per_step_local": local_elapsed / args.steps * 1e3,
                 **{k: st_acc[k] / args.steps for k in ("queries", "query_residues", "candidates", "hits")},
                 **{k.replace("seconds_", "ms_"): st_acc[k] / args.steps * 1e3
@@ -362,7 +418,7 @@ def main() -> None:
         hits = torch.tensor([sess.stats()["hits"]], device=coll_dev, dtype=torch.int64)
         dist.all_reduce(hits)
         if rank == 0:
-            gathered = b"".join(m.cpu().numpy().tobytes() for m in step.merged)
+            gathered = b"".join(m.cpu().numpy().tobytes() for m in gatherer.records())
             with Session(argv) as whole:
                 whole.run()
                 want_rec = whole.hits().tobytes()
@@ -397,11 +453,11 @@ def main() -> None:
             if dist is not None:
                 dist.barrier()
             te = time.perf_counter()
-            with open_session() as s2:
+            with guarded(open_session, "end-to-end session create") as s2:
                 if world == 1:
                     s2.run(to_file=True)  # the output file is written while the search runs
                 else:
-                    s2.run()
+                    guarded(s2.run, "end-to-end run")
                     write_assembled(dist, coll_dev, rank, world, out_path, s2.output())
                 # the output file is complete here; the session's teardown (device
                 # frees) is not part of the job, as at process exit
@@ -470,8 +526,10 @@ def main() -> None:
         dtype = ("int (exact 16-bit integers; packed f16 max3 orders their patterns, no guard)" if swar
                  else "int (exact integers in packed f16 lanes, int16 re-score above the guard)" if half
                  else "int16" if packed else "int32")
-        pmc = _json(PMC)
-        pmc_ok = bool(pmc and pmc.get("queries") == nq and world == 1 and preset == "cfg4" and not args.aln)
+        # the PMC summary of this preset's workload (tools/profile.sh <round> <preset>)
+        pmc = _json(os.path.join(REPO, "profiles", f"pmc_traffic_{preset}.json")) or _json(PMC)
+        pmc_ok = bool(pmc and pmc.get("queries") == nq and pmc.get("preset", "cfg4") == preset
+                      and world == 1 and not args.aln)
         issue = _json(VALU_ISSUE)
         roof = {
             "bound": "valu",

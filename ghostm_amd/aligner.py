@@ -142,6 +142,24 @@ class Session:
                 raise GhostmError(native.last_error())
         return out[: n * HIT_DTYPE.itemsize]
 
+    def device_hits_into(self, dst, cap: int) -> int:
+        """Copies the hit records of the last run device-to-device into `dst` (a
+        uint8 torch tensor on this session's GPU with room for `cap` records);
+        returns their number. Raises if there are more than `cap`."""
+        import torch
+
+        lib = native.load()
+        n = lib.GhostmSessionDeviceHits(self._h, None, 0)
+        if n == ctypes.c_size_t(-1).value:
+            raise GhostmError(native.last_error())
+        if n > cap or dst.numel() < n * HIT_DTYPE.itemsize:
+            raise GhostmError(f"{n} hit records do not fit the destination ({cap} records)")
+        if n:
+            torch.cuda.synchronize(dst.device)
+            if lib.GhostmSessionDeviceHits(self._h, ctypes.c_void_p(dst.data_ptr()), n) != n:
+                raise GhostmError(native.last_error())
+        return n
+
     def stats(self) -> dict:
         st = native.GhostmStats()
         # the sized call: a library built with more fields writes only ours

@@ -298,7 +298,7 @@ void Session::PrepareQueryChunk(QueryData *qd) {
 // The batch plan of a slice against DB chunk di, from the counts of its WHOLE
 // chunk: the unsharded run's batches (aligner.cpp:131-171, 511-514), which every
 // shard replays on its own queries (see Passes).
-void Session::PlanFromCounts(QueryData &q, size_t di, const std::vector<uint32_t> &chunk_counts) {
+void Session::PlanFromCounts(QueryData &q, size_t di, const std::vector<uint32_t> &chunk_counts, uint32_t n) {
   if (q.plan.size() <= di) {
     q.plan.resize(di + 1);
     q.plan_sum.resize(di + 1);
@@ -306,9 +306,9 @@ void Session::PlanFromCounts(QueryData &q, size_t di, const std::vector<uint32_t
   }
   q.plan[di] = CpuBatches(chunk_counts, opt_.max_list_length);
   uint64_t sum = 0;
-  for (uint32_t i = 0; i < q.chunk.nseq; ++i) sum += chunk_counts[q.slice_lo + i];
+  for (uint32_t i = 0; i < n; ++i) sum += chunk_counts[q.slice_lo + i];
   q.plan_sum[di] = sum;
-  q.plan_hash[di] = CountsHash(chunk_counts.data() + q.slice_lo, q.chunk.nseq);
+  q.plan_hash[di] = CountsHash(chunk_counts.data() + q.slice_lo, n);
   q.planned = true;
 }
 
@@ -348,18 +348,18 @@ void Session::ApplyShard(uint32_t rank, uint32_t world) {
       // the whole chunk's counts against every DB chunk -> its batch plan
       q.slice_lo = i0;
       q.chunk_nseq = c.nseq;
-      DevQuery *full = dev.UploadQuery(c.seq.data(), c.nseq, c.L);
-      std::vector<uint32_t> counts;
-      std::vector<uint64_t> offsets;
-      const uint32_t whole = c.nseq;
-      c.nseq = n;  // PlanFromCounts reads the slice's size
-      for (size_t di = 0; di < dbs_.size(); ++di) {
-        sc.seed_mask = dbs_[di].chunk.seed;
-        dev.Seed(full, dbs_[di].dev, sc, &counts, &offsets);
-        PlanFromCounts(q, di, counts);
+      {
+        // the whole chunk on the device while it is counted; freed on every exit
+        std::unique_ptr<DevQuery, std::function<void(DevQuery *)>> full(
+            dev.UploadQuery(c.seq.data(), c.nseq, c.L), [&dev](DevQuery *p) { dev.Free(p); });
+        std::vector<uint32_t> counts;
+        std::vector<uint64_t> offsets;
+        for (size_t di = 0; di < dbs_.size(); ++di) {
+          sc.seed_mask = dbs_[di].chunk.seed;
+          dev.Seed(full.get(), dbs_[di].dev, sc, &counts, &offsets);
+          PlanFromCounts(q, di, counts, n);
+        }
       }
-      c.nseq = whole;
-      dev.Free(full);
       c.seq.Own(std::vector<uint8_t>(c.seq.begin() + (size_t)i0 * c.L, c.seq.begin() + (size_t)(i0 + n) * c.L));
       c.names = std::vector<std::string>(c.names.begin() + i0, c.names.begin() + i0 + n);
       c.nseq = n;
@@ -396,23 +396,38 @@ void Session::PlanExchange(uint32_t rank, uint32_t world, const ShardExchange &e
     if (k != queries_.size()) throw Error("shard slices out of order");
   }
   std::vector<std::vector<uint32_t>> mine(nc * nd);
-  std::vector<uint64_t> sums(nc * nd, 0);
-  for (size_t c = 0; c < nc; ++c) {
-    if (!slice[c]) continue;
-    std::vector<uint64_t> offsets;
-    for (size_t di = 0; di < nd; ++di) {
-      sc.seed_mask = dbs_[di].chunk.seed;
-      sums[c * nd + di] = dev.Seed(slice[c]->dev, dbs_[di].dev, sc, &mine[c * nd + di], &offsets);
+  // the candidate totals per (chunk, DB chunk), then this rank's ok flag: a
+  // rank whose counting fails still takes part in the gather, and every rank
+  // then fails
+  const size_t np = nc * nd;
+  std::vector<uint64_t> sums(np + 1, 0);
+  std::string err;
+  try {
+    for (size_t c = 0; c < nc; ++c) {
+      if (!slice[c]) continue;
+      std::vector<uint64_t> offsets;
+      for (size_t di = 0; di < nd; ++di) {
+        sc.seed_mask = dbs_[di].chunk.seed;
+        sums[c * nd + di] = dev.Seed(slice[c]->dev, dbs_[di].dev, sc, &mine[c * nd + di], &offsets);
+      }
     }
+  } catch (std::exception &e) {
+    err = e.what();
+    if (err.empty()) err = "shard session: counting failed";
   }
+  sums[np] = err.empty() ? 1 : 0;
   auto gather = [&](const void *send, uint64_t bytes, void *recv, const std::vector<uint64_t> &sizes) {
     if (ex.fn(ex.ctx, send, bytes, recv, sizes.data()) != 0) throw Error("shard exchange (all-gather) failed");
   };
-  std::vector<uint64_t> all(world * nc * nd);
+  std::vector<uint64_t> all(world * (np + 1));
   gather(sums.data(), sums.size() * 8, all.data(), std::vector<uint64_t>(world, sums.size() * 8));
-  std::vector<uint64_t> total(nc * nd, 0);
+  if (!err.empty()) throw Error(err);
   for (uint32_t r = 0; r < world; ++r)
-    for (size_t p = 0; p < nc * nd; ++p) total[p] += all[r * nc * nd + p];
+    if (all[r * (np + 1) + np] != 1)
+      throw Error("shard session: rank " + std::to_string(r) + " failed counting its queries");
+  std::vector<uint64_t> total(np, 0);
+  for (uint32_t r = 0; r < world; ++r)
+    for (size_t p = 0; p < np; ++p) total[p] += all[r * (np + 1) + p];
   // pairs that need the whole chunk's counts: more than one batch
   std::vector<size_t> wide;
   for (size_t p = 0; p < nc * nd; ++p)
@@ -486,6 +501,74 @@ Session::Session(const AlignerOptions &opt, uint32_t shard_rank, uint32_t shard_
   if (shard_world == 0 || shard_rank >= shard_world) throw std::invalid_argument("shard rank outside the world");
   shard_world_ = shard_world;
   const bool local = shard_world > 1 && ex && ex->fn;  // rank-local reads + exchange
+  std::vector<uint32_t> chunk_nseq;
+  std::vector<std::vector<uint64_t>> rank_lo;
+  if (!local) {
+    Load(shard_rank, shard_world, false, &chunk_nseq, &rank_lo);
+  } else {
+    // a rank whose loading fails still joins the creation header exchange with
+    // its error flag set, so every rank fails together instead of its peers
+    // waiting in the plan's all-gather for a rank that never comes
+    std::string err;
+    try {
+      Load(shard_rank, shard_world, true, &chunk_nseq, &rank_lo);
+    } catch (std::exception &e) {
+      err = e.what();
+      if (err.empty()) err = "shard session creation failed";
+    }
+    AgreeOnCreate(shard_rank, shard_world, *ex, err, chunk_nseq, rank_lo);
+    PlanExchange(shard_rank, shard_world, *ex, chunk_nseq, rank_lo);
+  }
+  DeviceModule::Get().Synchronize();
+  TraceMark("uploaded");
+  formatter_.reset(new TaskQueue());
+}
+
+// Every rank's view of the job must be the same before the plan's all-gather
+// sizes its buffers from it: a fixed-size header per rank (ok flag, query
+// chunks, DB chunks, queries, a hash of every chunk's size and of the shard
+// cuts) is all-gathered first. Any rank's failure or any disagreement throws on
+// every rank.
+void Session::AgreeOnCreate(uint32_t rank, uint32_t world, const ShardExchange &ex, const std::string &err,
+                            const std::vector<uint32_t> &chunk_nseq,
+                            const std::vector<std::vector<uint64_t>> &rank_lo) {
+  constexpr size_t kWords = 8;
+  uint64_t mine[kWords] = {0};
+  mine[0] = err.empty() ? 1 : 0;
+  if (err.empty()) {
+    mine[1] = chunk_nseq.size();
+    mine[2] = dbs_.size();
+    for (uint32_t n : chunk_nseq) mine[3] += n;
+    mine[4] = CountsHash(chunk_nseq.data(), chunk_nseq.size());
+    std::vector<uint32_t> cuts;
+    for (const std::vector<uint64_t> &lo : rank_lo)
+      for (uint64_t x : lo) cuts.push_back((uint32_t)x);
+    mine[5] = CountsHash(cuts.data(), cuts.size());
+    mine[6] = db_sum_u32_;
+    mine[7] = world;
+  }
+  std::vector<uint64_t> all(world * kWords);
+  const std::vector<uint64_t> sizes(world, sizeof(mine));
+  if (ex.fn(ex.ctx, mine, sizeof(mine), all.data(), sizes.data()) != 0)
+    throw Error("shard exchange (creation header all-gather) failed");
+  if (!err.empty()) throw Error(err);
+  for (uint32_t r = 0; r < world; ++r) {
+    const uint64_t *h = &all[r * kWords];
+    if (h[0] != 1) throw Error("shard session: rank " + std::to_string(r) + " failed at creation");
+    for (size_t k = 1; k < kWords; ++k)
+      if (h[k] != mine[k])
+        throw Error("shard session: rank " + std::to_string(r) + " sees a different query/DB set than rank " +
+                    std::to_string(rank));
+  }
+}
+
+// Reads and uploads the query and DB chunks (a rank-local shard: only its own
+// slice of the queries) and, for a rank-local shard, returns the chunks' sizes
+// and every rank's first query per chunk.
+void Session::Load(uint32_t shard_rank, uint32_t shard_world, bool local, std::vector<uint32_t> *chunk_nseq_out,
+                   std::vector<std::vector<uint64_t>> *rank_lo_out) {
+  std::vector<uint32_t> &chunk_nseq = *chunk_nseq_out;
+  std::vector<std::vector<uint64_t>> &rank_lo = *rank_lo_out;
   DeviceModule &dev = DeviceModule::Get();
   TraceMark("create");
   dev.Bind(opt_.device);
@@ -563,8 +646,6 @@ Session::Session(const AlignerOptions &opt, uint32_t shard_rank, uint32_t shard_
     dev.SetChunkBases(bases.data(), (uint32_t)bases.size());
   }
 
-  std::vector<uint32_t> chunk_nseq;
-  std::vector<std::vector<uint64_t>> rank_lo;
   if (local) {
     // the cut over every selected query from the chunk indices, then only this
     // rank's rows and names are read
@@ -622,10 +703,6 @@ Session::Session(const AlignerOptions &opt, uint32_t shard_rank, uint32_t shard_
     dev.SetQueryGroups(q.dev, q.group_first.data(), q.group_last.data(), (uint32_t)q.group_first.size());
     q.chunk.seq.Release();  // resident on the device (qlen and names stay on the host)
   }
-  if (local) PlanExchange(shard_rank, shard_world, *ex, chunk_nseq, rank_lo);
-  dev.Synchronize();
-  TraceMark("uploaded");
-  formatter_.reset(new TaskQueue());
 }
 
 namespace {

@@ -69,7 +69,7 @@ struct HitRecord {
 
 // Number of host worker threads: GHOSTM_THREADS, else this process's share of
 // the CPUs it may run on (affinity mask, cgroup quota) divided among the ranks
-// of this node (LOCAL_WORLD_SIZE), between 2 and 16.
+// of this node (LOCAL_WORLD_SIZE), between 1 and 16.
 unsigned HostThreads();
 
 // One batch of the reference's batch loop (aligner.cpp:131-171 with
@@ -177,7 +177,11 @@ class Session {
   static void PrepareQueryChunk(QueryData *q);
   void ApplyShard(uint32_t rank, uint32_t world);
   // shard sessions: the batch plan of every (query chunk, DB chunk)
-  void PlanFromCounts(QueryData &q, size_t di, const std::vector<uint32_t> &chunk_counts);
+  void PlanFromCounts(QueryData &q, size_t di, const std::vector<uint32_t> &chunk_counts, uint32_t n);
+  void Load(uint32_t shard_rank, uint32_t shard_world, bool local, std::vector<uint32_t> *chunk_nseq,
+            std::vector<std::vector<uint64_t>> *rank_lo);
+  void AgreeOnCreate(uint32_t rank, uint32_t world, const ShardExchange &ex, const std::string &err,
+                     const std::vector<uint32_t> &chunk_nseq, const std::vector<std::vector<uint64_t>> &rank_lo);
   void PlanExchange(uint32_t rank, uint32_t world, const ShardExchange &ex,
                     const std::vector<uint32_t> &chunk_nseq, const std::vector<std::vector<uint64_t>> &rank_lo);
   // the passes of one Seed() result: the plan's batches restricted to the

@@ -2452,16 +2452,22 @@ __device__ inline void MergeWaveGroup(const MergeArgs &a, uint32_t g, uint32_t l
     }
     // first occurrence by lane order: the lanes holding the same subject, from
     // one ballot per subject-index bit (sid < nsubj; carried lanes and lanes
-    // past m hold kNoSlot and take no part)
+    // past m hold kNoSlot and take no part). A new candidate whose end maps to
+    // no subject (sid >= nsubj, i.e. kNoSlot) compares equal only to its own
+    // kind, as the full-sid compare of MergeGroup does: one more ballot.
     {
-      const bool real = lane < m && !carried;
+      const bool fresh = lane < m && !carried;
+      const bool real = fresh && sid < a.nsubj;
+      const bool stray = fresh && sid >= a.nsubj;
       unsigned long long peers = __ballot(real);
       for (uint32_t bit = 0; bit < a.sid_bits; ++bit) {
         const bool one = (sid >> bit) & 1u;
         const unsigned long long bal = __ballot(one);
         peers &= one ? bal : ~bal;
       }
-      if (real && (peers & ((1ull << lane) - 1))) ok = false;
+      const unsigned long long strays = __ballot(stray);
+      const unsigned long long before = (1ull << lane) - 1;
+      if ((real && (peers & before)) || (stray && (strays & before))) ok = false;
     }
     const unsigned long long bal = __ballot(ok);
     const uint32_t rank = __popcll(bal & ((1ull << lane) - 1));

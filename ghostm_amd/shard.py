@@ -68,6 +68,53 @@ def gather_device_records(payload, dist, itemsize: int):
     return [g[: int(s.item())] for g, s in zip(gathered, sizes)]
 
 
+class RecordGather:
+    """The single data-path collective of a step: every rank
+    sends a fixed-capacity buffer of `cap` 32-byte hit records plus one header
+    record (its count), and rank 0 receives all of them in one gather — no size
+    exchange first, since cap (shard queries x -b, the most a shard can return)
+    is fixed for the session. The buffers are allocated once."""
+
+    def __init__(self, dist, cap_records: int, itemsize: int, device):
+        import torch
+
+        self.dist = dist
+        self.itemsize = itemsize
+        self.cap = int(cap_records)
+        self.world = dist.get_world_size()
+        self.rank = dist.get_rank()
+        self.buf = torch.zeros((self.cap + 1) * itemsize, dtype=torch.uint8, device=device)
+        self.parts = [torch.empty_like(self.buf) for _ in range(self.world)] if self.rank == 0 else None
+
+    def payload(self):
+        """The record area (cap records), to be filled in place."""
+        return self.buf[self.itemsize:]
+
+    def set_count(self, n: int) -> None:
+        import torch
+
+        if n > self.cap:
+            raise ValueError(f"{n} hit records exceed the gather capacity {self.cap}")
+        self.buf[:8].copy_(torch.tensor([n], dtype=torch.int64).view(torch.uint8))
+
+    def gather(self) -> None:
+        self.dist.gather(self.buf, self.parts, dst=0)
+
+    def records(self):
+        """Rank 0: every rank's records (uint8 tensors, device) in rank order."""
+        import torch
+
+        if self.parts is None:
+            return None
+        out = []
+        for p in self.parts:
+            n = int(p[:8].cpu().view(torch.int64)[0])
+            if n > self.cap:
+                raise ValueError("gathered header exceeds the capacity")
+            out.append(p[self.itemsize: self.itemsize + n * self.itemsize])
+        return out
+
+
 def gather_hits(hits: np.ndarray, dist, device) -> list[np.ndarray] | None:
     """Gather every rank's hit records (a structured array of any dtype) to rank 0.
     Returns the per-rank arrays in rank order on rank 0, None elsewhere. Sizes

@@ -47,6 +47,24 @@ for _g, _e in ((8, 1), (8, 2), (10, 1), (10, 2), (11, 2), (14, 1), (14, 2)):
         WORKLOADS["cfg5"], aln=["-r", "64", "-M", PAM250, "-G", str(_g), "-E", str(_e), "-y", "2"],
         workload=f"cfg5 gap sweep: -r 64, PAM250 {_g}/{_e}, -y 2; synthetic 100k queries x 5M-residue DB")
 
+# Multi-batch pins: the reference's batch loop (aligner.cpp:131-171,
+# 383-391, 511-514) cut by a real `-l 1` (2^20 candidates per batch), run as ONE
+# reference process, since the cuts depend on the whole query chunk. The first
+# 20k cfg4 queries have ~2.5 M candidates (3 batches); the DNA set's six-frame
+# name groups are split by batch cuts.
+_CFG4_20K = dict(WORKLOADS["cfg4"], queries=20_000, single_process=True)
+WORKLOADS["cfg4_20k_l1"] = dict(_CFG4_20K, aln=["-l", "1"],
+                                workload="first 20k cfg4 queries x 10M-residue DB, -l 1 (multi-batch)")
+WORKLOADS["cfg4_20k_l1_b20y2"] = dict(_CFG4_20K, aln=["-l", "1", "-b", "20", "-y", "2"],
+                                      workload="first 20k cfg4 queries x 10M-residue DB, -l 1 -b 20 -y 2")
+_DNA = {"synth": ["-s", "21", "-N", "5000000", "-t", "dna", "-l", "300"], "queries": 40_000,
+        "db": ("synth", 5_000_000, 21), "qry": ["-t", "d", "-l", "300"], "single_process": True,
+        "cpu_sample": 2000, "cpu_sample_all": 4000}
+WORKLOADS["dna40k_l1"] = dict(_DNA, aln=["-l", "1"],
+                              workload="40k DNA reads (300 nt, six frames) x 5M-residue DB, -l 1 (multi-batch)")
+WORKLOADS["dna40k_l1_b20"] = dict(_DNA, aln=["-l", "1", "-b", "20"],
+                                  workload="40k DNA reads (300 nt, six frames) x 5M-residue DB, -l 1 -b 20")
+
 
 def _run(exe: str, *args: str) -> None:
     subprocess.run([exe, *args], check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)

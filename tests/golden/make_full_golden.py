@@ -42,8 +42,51 @@ def run(*a, **kw):
     return subprocess.run(list(a), check=True, capture_output=True, **kw)
 
 
+def single_process_output(name: str, tmp: str) -> dict:
+    """One reference process over the whole query set (the multi-batch pins:
+    batch cuts depend on the whole chunk), with -v, whose per-batch log lines
+    give the number of batches the reference ran."""
+    w = WORKLOADS[name]
+    root = os.path.join(tmp, name)
+    db = make_db(name, os.path.join(root, "db"), exe=cases.REF)
+    n = w["queries"]
+    q = make_queries(name, os.path.join(root, "q"), 0, n, exe=cases.REF)
+    t0 = time.time()
+    log = run("nice", "-n", "5", cases.REF, "aln", "-i", q, "-d", db, "-o", f"{root}/out", "-v", *w["aln"]).stdout
+    wall = time.time() - t0
+    batches = log.count(b"|Calculate scores")
+    h = hashlib.sha256()
+    with open(f"{root}/out", "rb") as f:
+        data = f.read()
+    h.update(data)
+    return {"sha256": h.hexdigest(), "lines": data.count(b"\n"), "bytes": len(data), "queries": n,
+            "query_synth": ["-n", str(n)] + [os.path.basename(x) if x in (TESTSET_DB, PAM250) else x
+                                              for x in w["synth"]],
+            "db": [os.path.basename(x) if isinstance(x, str) and os.path.isabs(x) else x for x in w["db"]],
+            "qry": w["qry"],
+            "aln": [os.path.basename(x) if x == PAM250 else x for x in w["aln"]],
+            "reference_batches": batches,
+            "reference_processes": 1, "reference_wall_s": round(wall, 1)}
+
+
+def restatement_check(name: str, pin: dict, tmp: str) -> bool:
+    """The builder's CPU restatement (oracle/_build/ghostm_oracle) on the same
+    single-process workload, against the reference pin."""
+    w = WORKLOADS[name]
+    root = os.path.join(tmp, name + "_restated")
+    db = make_db(name, os.path.join(root, "db"))
+    q = make_queries(name, os.path.join(root, "q"), 0, w["queries"])
+    run("nice", "-n", "5", cases.ORACLE, "aln", "-i", q, "-d", db, "-o", f"{root}/out", *w["aln"])
+    h = hashlib.sha256()
+    with open(f"{root}/out", "rb") as f:
+        h.update(f.read())
+    return h.hexdigest() == pin["sha256"]
+
+
 def reference_output(name: str, procs: int, tmp: str) -> dict:
     w = WORKLOADS[name]
+    if w.get("single_process"):
+        return single_process_output(name, tmp)
     root = os.path.join(tmp, name)
     db = make_db(name, os.path.join(root, "db"), exe=cases.REF)
     n = w["queries"]
@@ -95,6 +138,8 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("names", nargs="+", choices=sorted(WORKLOADS))
     ap.add_argument("-P", type=int, default=6)
+    ap.add_argument("--check-restatement", action="store_true",
+                    help="only run the restatement on already pinned single-process workloads")
     args = ap.parse_args()
     if not os.path.exists(cases.REF):
         raise SystemExit("oracle/_ref/ghostm_ref missing: make -C oracle ref")
@@ -105,12 +150,39 @@ def main() -> None:
     data.setdefault("generator", "tests/golden/make_full_golden.py")
     data.setdefault("reference", "oracle/_ref/ghostm_ref (reference CPU path, g++ -O2), P query-range processes")
     tmp = tempfile.mkdtemp(prefix="ghostm_full_golden_", dir=os.environ.get("GHOSTM_GOLDEN_TMP"))
-    for name in args.names:
-        t = time.time()
-        data[name] = reference_output(name, args.P, tmp)
-        print(f"{name}: {data[name]['lines']} lines, {time.time() - t:.0f} s", flush=True)
+    if args.check_restatement:
+        from concurrent.futures import ThreadPoolExecutor
+
+        names = [n for n in args.names if n in data]
+        with ThreadPoolExecutor(max(1, min(len(names), args.P))) as pool:
+            oks = list(pool.map(lambda n: restatement_check(n, data[n], tmp), names))
+        for n, ok in zip(names, oks):
+            print(f"{n}: restatement {'equals' if ok else 'DIFFERS FROM'} the reference pin", flush=True)
+            data[n]["restatement_matches"] = ok
         with open(OUT, "w") as f:
             json.dump(data, f, indent=1, sort_keys=True)
+        subprocess.run(["rm", "-rf", tmp])
+        return
+    # single-process pins run side by side (one reference process each); the
+    # split pins one after another (each uses P processes)
+    single = [n for n in args.names if WORKLOADS[n].get("single_process")]
+    split = [n for n in args.names if n not in single]
+
+    def one(name):
+        t = time.time()
+        res = reference_output(name, args.P, tmp)
+        print(f"{name}: {res['lines']} lines, {time.time() - t:.0f} s", flush=True)
+        return name, res
+
+    from concurrent.futures import ThreadPoolExecutor
+
+    with ThreadPoolExecutor(max(1, min(len(single), args.P))) as pool:
+        results = list(pool.map(one, single))
+    results += [one(n) for n in split]
+    for name, res in results:
+        data[name] = res
+    with open(OUT, "w") as f:
+        json.dump(data, f, indent=1, sort_keys=True)
     subprocess.run(["rm", "-rf", tmp])
 
 

@@ -183,8 +183,12 @@ def _full_pins():
         return {k: v for k, v in json.load(f).items() if isinstance(v, dict)}
 
 
+MULTI_BATCH = ["cfg4_20k_l1", "cfg4_20k_l1_b20y2", "dna40k_l1", "dna40k_l1_b20"]
+
+
 @pytest.mark.parametrize("name", ["cfg2", "cfg3", "cfg5", "cfg4"] + sorted(n for n in workloads.WORKLOADS
-                                                                            if n.startswith("cfg5_g")))
+                                                                            if n.startswith("cfg5_g"))
+                         + MULTI_BATCH)
 def test_full_workload_matches_reference(name, tmp_path):
     """The complete BASELINE workload, formatted here and searched by the HIP
     path, against the reference CPU program's full output (sha256, lines)."""
@@ -204,12 +208,15 @@ def test_full_workload_matches_reference(name, tmp_path):
     assert st["queries"] == pin["queries"]
 
 
-@pytest.mark.parametrize("name,world", [("cfg4", 8), ("cfg3", 3)])
+@pytest.mark.parametrize("name,world", [("cfg4", 8), ("cfg3", 3), ("cfg4_20k_l1", 3), ("cfg4_20k_l1", 8),
+                                        ("cfg4_20k_l1_b20y2", 8), ("dna40k_l1", 3), ("dna40k_l1_b20", 8)])
 def test_full_workload_sharded_matches_reference(name, world, tmp_path):
     """The headline workload as the driver's 8-GPU run cuts it: `world` shard
     sessions (GhostmSessionCreateShard, one after another on this GPU), their
     outputs concatenated in rank order against the reference CPU program's
-    full output, and their records against the unsharded run's."""
+    full output, and their records against the unsharded run's. The `_l1`
+    workloads run several batches (`-l 1`), pinned by ONE reference process:
+    every shard replays the unsharded batch cuts."""
     pin = _full_pins().get(name)
     if pin is None:
         pytest.skip(f"{name} not pinned in full_golden.json")

@@ -290,3 +290,65 @@ def test_rank_local_names_file_shorter_than_the_chunk(dataset, tmp_path):
     text, got, _ = _run_ranks(tmp_path, str(d), 3, [], {}, True)
     assert text == want
     assert got.tobytes() == want_hits.tobytes()
+
+
+FAIL_RANK = textwrap.dedent("""
+    import datetime, sys
+    import torch.distributed as dist
+    sys.path.insert(0, {repo!r})
+    from ghostm_amd.aligner import Session
+    from ghostm_amd.shard import torch_allgather
+    rank, world, d, other = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
+    mode = sys.argv[5]
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=240))
+    q, db = d + "/q", d + "/db"
+    if rank == 1 and mode == "missing_db":
+        db = d + "/no_such_db"
+    if rank == 1 and mode == "other_queries":
+        q = other + "/q"
+    try:
+        Session(["-i", q, "-d", db, "-o", d + "/x", "-D", "0"], shard=(rank, world), exchange=torch_allgather(dist))
+    except Exception as e:
+        print("create failed:", e, flush=True)
+        sys.exit(3)
+    print("create succeeded", flush=True)
+""")
+
+
+@pytest.mark.parametrize("mode,msg", [("missing_db", "failed at creation"),
+                                      ("other_queries", "sees a different query/DB set")])
+def test_rank_local_creation_fails_on_every_rank(mode, msg, dataset, tmp_path):
+    """One rank that cannot load (a missing DB) or that sees another query set
+    makes every rank's GhostmSessionCreateShardEx fail through the creation
+    header exchange, instead of its peers waiting in the plan's all-gather."""
+    d, other = dataset("syn_small"), dataset("syn_dna")
+    script = tmp_path / "fail_rank.py"
+    script.write_text(FAIL_RANK.format(repo=cases.REPO))
+    e = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    procs = [subprocess.Popen([sys.executable, str(script), str(r), "3", d, other, mode], env=e,
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(3)]
+    logs = [p.communicate(timeout=200)[0].decode() for p in procs]
+    assert all(p.returncode == 3 for p in procs), "\n".join(logs)
+    for r, log in enumerate(logs):
+        if r != 1:
+            assert msg in log, log
+
+
+@pytest.mark.parametrize("name,world", [("cfg4_20k_l1_b20y2", 3), ("dna40k_l1_b20", 8)])
+def test_rank_local_multi_batch_matches_reference_pin(name, world, tmp_path):
+    """Rank-local shard sessions over gloo (GhostmSessionCreateShardEx, every
+    rank on cuda:0) on a workload the reference cut into several batches
+    (`-l 1`, one reference process): the gathered text is the reference's."""
+    from ghostm_amd import workloads
+
+    with open(os.path.join(cases.GOLDEN, "full_golden.json")) as f:
+        pin = json.load(f).get(name)
+    if pin is None:
+        pytest.skip(f"{name} not pinned")
+    d = str(tmp_path / "ds")
+    workloads.make_db(name, d)
+    workloads.make_queries(name, d)
+    text, got, ranges = _run_ranks(tmp_path, d, world, workloads.WORKLOADS[name]["aln"], {}, True)
+    assert len(text) == pin["bytes"]
+    assert _sha(text) == pin["sha256"]
+    assert ranges[0][0] == 0 and all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))

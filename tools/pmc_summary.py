@@ -58,6 +58,7 @@ def main() -> None:
     ap.add_argument("--round", required=True)
     ap.add_argument("--prof", required=True)
     ap.add_argument("--queries", type=int, required=True)
+    ap.add_argument("--preset", default="cfg4", help="bench preset profiled (pmc_traffic_<preset>.json)")
     ap.add_argument("--trace-runs", type=int, default=3, help="session runs in the traced command (warmup + steps)")
     args = ap.parse_args()
     prof = os.path.join(REPO, "profiles")
@@ -116,7 +117,8 @@ def main() -> None:
                 busy = c["SQ_LDS_IDX_ACTIVE"] - c["SQ_LDS_BANK_CONFLICT"]
                 e["lds_bank_conflict_rate"] = c["SQ_LDS_BANK_CONFLICT"] / busy if busy > 0 else None
     with open(os.path.join(prof, f"{args.round}_pmc.json"), "w") as f:
-        json.dump({"round": args.round, "queries": args.queries, "kernels": kernels}, f, indent=1, sort_keys=True)
+        json.dump({"round": args.round, "queries": args.queries, "preset": args.preset, "kernels": kernels}, f,
+                  indent=1, sort_keys=True)
 
     def fam(prefix):
         best = [k for k in kernels if k.startswith(prefix) and "hbm_bytes_per_launch" in kernels[k]]
@@ -133,7 +135,7 @@ def main() -> None:
     k1v_step = sum(kernels[k]["valu_insts_per_launch"] * kernels[k].get("launches_in_trace", 0) for k in k1v)
     k2 = [k for k in kernels if k.startswith("k_score") and "valu_insts_per_launch" in kernels[k]]
     k2_main = max(k2, key=lambda x: kernels[x].get("percent_of_gpu_time", 0)) if k2 else None
-    traffic = {"round": args.round, "queries": args.queries,
+    traffic = {"round": args.round, "queries": args.queries, "preset": args.preset,
                "note": "HBM bytes per launch = FETCH_SIZE*2*1024 + WRITE_SIZE*1024 (gfx950 correction); "
                        "VALU instructions = SQ_INSTS_VALU per dispatch",
                "k_score_hbm_bytes_per_launch": fam("k_score"),
@@ -146,8 +148,10 @@ def main() -> None:
                "k1_hbm_bytes_per_step": k1_step / args.trace_runs if k1 else None,
                "k1_valu_insts_per_step": k1v_step / args.trace_runs if k1v else None,
                "k1_kernels": sorted(k1)}
-    with open(os.path.join(prof, "pmc_traffic.json"), "w") as f:
-        json.dump(traffic, f, indent=1)
+    names = [f"pmc_traffic_{args.preset}.json"] + (["pmc_traffic.json"] if args.preset == "cfg4" else [])
+    for name in names:
+        with open(os.path.join(prof, name), "w") as f:
+            json.dump(traffic, f, indent=1)
     print(json.dumps(traffic))
 
 
