@@ -794,7 +794,8 @@ void DeviceModule::CopyStarts(uint64_t begin, uint64_t n, uint32_t *out) {
 // its first touch cost more than the loop). A task closes when full, when it
 // spans Qmax queries, or at the end, so ScoreTaskBound is an upper bound.
 static size_t ScoreTaskBound(uint64_t n, uint32_t q_first, uint32_t q_end, uint32_t per_block, uint32_t qmax) {
-  return (size_t)(n / per_block) + (q_end - q_first) / qmax + 2;
+  // paired unit tasks: full blocks plus at most one remainder task per query
+  return (size_t)(n / per_block) + (q_end - q_first) + 2;
 }
 static size_t BuildScoreTasks(uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32_t q_end,
                               const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets,
@@ -821,11 +822,107 @@ static size_t BuildScoreTasks(uint64_t cand_begin, uint64_t n, uint32_t q_first,
       const uint64_t take = std::min<uint64_t>(hi - lo, per_block - cur.count);
       cur.count += (uint32_t)take;
       cur.q_count = qi - cur.q_first + 1;
+      cur.count1 = cur.count;
+      cur.begin2 = cur.begin + cur.count;
+      cur.q_second = cur.q_first + 1;
       lo += take;
     }
   }
   flush();
   return nt;
+}
+
+// Tasks of k_score16f's unit-pair kernel (two query profiles per block): each
+// query's candidates in full blocks of per_block, and the remainders paired two
+// queries to a block, so that the pair fills fewer waves than the two alone
+// would. A wave (64 lanes, `wave_slots` candidates) costs the same however few
+// of its candidates are real, so a remainder of r costs ceil(r / wave_slots)
+// waves; two remainders whose partial waves fit one wave together save one.
+// Each remainder takes the largest partner that saves a wave (best fit by the
+// partial wave's size), else runs alone. At 63 candidates per query (cfg 3)
+// consecutive pairs of queries left 8 % more waves than four queries per block.
+static size_t BuildScoreTasksPaired(uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32_t q_end,
+                                    const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets,
+                                    uint32_t per_block, uint32_t wave_slots, kern::ScoreTask *out) {
+  size_t nt = 0;
+  auto single = [&](uint32_t q, uint64_t begin, uint32_t count) {
+    kern::ScoreTask t{};
+    t.begin = begin;
+    t.count = count;
+    t.count1 = count;
+    t.q_first = q;
+    t.q_count = 1;
+    t.begin2 = begin + count;
+    t.q_second = q;
+    out[nt++] = t;
+  };
+  // remainders by size (1 .. per_block - 1): stacks of (query, first candidate)
+  std::vector<std::vector<std::pair<uint32_t, uint64_t>>> rem(per_block);
+  const uint64_t cand_end = cand_begin + n;
+  for (uint32_t qi = q_first; qi < q_end; ++qi) {
+    uint64_t lo = std::max<uint64_t>(offsets[qi], cand_begin);
+    const uint64_t hi = std::min<uint64_t>(offsets[qi] + counts[qi], cand_end);
+    if (lo >= hi) continue;
+    while (hi - lo >= per_block) {
+      single(qi, lo, per_block);
+      lo += per_block;
+    }
+    if (hi > lo) rem[hi - lo].emplace_back(qi, lo);
+  }
+  auto partial = [&](uint32_t r) { return r - (r - 1) / wave_slots * wave_slots; };  // 1 .. wave_slots
+  for (uint32_t r1 = per_block - 1; r1 >= 1; --r1) {
+    while (!rem[r1].empty()) {
+      const std::pair<uint32_t, uint64_t> a = rem[r1].back();
+      rem[r1].pop_back();
+      // the partner with the largest partial wave that still fits beside r1's
+      const uint32_t room = wave_slots - partial(r1);
+      uint32_t pick = 0;
+      for (uint32_t p = room; p >= 1 && !pick; --p)
+        for (uint32_t r2 = p; r2 <= r1 && r1 + r2 <= per_block; r2 += wave_slots)
+          if (!rem[r2].empty()) pick = r2;  // the largest with this partial wave
+      if (!pick) {
+        single(a.first, a.second, r1);
+        continue;
+      }
+      const std::pair<uint32_t, uint64_t> b = rem[pick].back();
+      rem[pick].pop_back();
+      kern::ScoreTask t{};
+      t.begin = a.second;
+      t.count1 = r1;
+      t.q_first = a.first;
+      t.begin2 = b.second;
+      t.q_second = b.first;
+      t.count = r1 + pick;
+      t.q_count = 2;
+      out[nt++] = t;
+    }
+  }
+  return nt;
+}
+
+// The unit kernel takes whichever of the paired and the consecutive tasks
+// fill fewer waves (consecutive runs win narrowly near 127 candidates per
+// query, pairs clearly at 63); GHOSTM_K2_TASKS=paired|consecutive forces one.
+static size_t BuildTasks(bool unit, uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32_t q_end,
+                         const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets,
+                         uint32_t per_block, uint32_t qmax, uint32_t wave_slots, kern::ScoreTask *out) {
+  if (!unit) return BuildScoreTasks(cand_begin, n, q_first, q_end, counts, offsets, per_block, qmax, out);
+  const char *force = getenv("GHOSTM_K2_TASKS");
+  if (force && strcmp(force, "consecutive") == 0)
+    return BuildScoreTasks(cand_begin, n, q_first, q_end, counts, offsets, per_block, qmax, out);
+  const size_t np = BuildScoreTasksPaired(cand_begin, n, q_first, q_end, counts, offsets, per_block, wave_slots, out);
+  if (force && strcmp(force, "paired") == 0) return np;
+  auto waves = [&](const kern::ScoreTask *t, size_t nt) {
+    uint64_t w = 0;
+    for (size_t k = 0; k < nt; ++k) w += (t[k].count + wave_slots - 1) / wave_slots;
+    return w;
+  };
+  std::vector<kern::ScoreTask> consecutive(ScoreTaskBound(n, q_first, q_end, per_block, qmax));
+  const size_t nc = BuildScoreTasks(cand_begin, n, q_first, q_end, counts, offsets, per_block, qmax,
+                                    consecutive.data());
+  if (waves(consecutive.data(), nc) >= waves(out, np)) return np;
+  std::copy(consecutive.begin(), consecutive.begin() + nc, out);
+  return nc;
 }
 
 // k_score16f's unit-pair kernel (UNIT) holds the profiles of kScoreQmaxUnit
@@ -923,8 +1020,8 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
     // a launch that has been waited for, so the copy needs no wait either
     PinnedBuf &hs = I.h_tasks[buf];
     hs.Reserve(ScoreTaskBound(n, q_first, q_end, per_block, qmax) * sizeof(kern::ScoreTask));
-    ntasks = BuildScoreTasks(cand_begin, n, q_first, q_end, counts, offsets, per_block, qmax,
-                             hs.as<kern::ScoreTask>());
+    ntasks = BuildTasks(unit, cand_begin, n, q_first, q_end, counts, offsets, per_block, qmax, per_block / 4,
+                        hs.as<kern::ScoreTask>());
     TraceMark("tasks", ntasks);
     const size_t tb = ntasks * sizeof(kern::ScoreTask);
     I.task_buf[buf].Reserve(tb);
@@ -1025,11 +1122,11 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
   if (next && next->n) {
     const int nb = I.task_turn;
     PinnedBuf &hs = I.h_tasks[nb];
-    const uint32_t nqmax = ScoreUnit(swar, next->n, next->q_first, next->q_end) ? kern::kScoreQmaxUnit
-                                                                                 : kern::kScoreQmax;
+    const bool nunit = ScoreUnit(swar, next->n, next->q_first, next->q_end);
+    const uint32_t nqmax = nunit ? kern::kScoreQmaxUnit : kern::kScoreQmax;
     hs.Reserve(ScoreTaskBound(next->n, next->q_first, next->q_end, per_block, nqmax) * sizeof(kern::ScoreTask));
-    const size_t nt = BuildScoreTasks(next->cand_begin, next->n, next->q_first, next->q_end, counts, offsets,
-                                      per_block, nqmax, hs.as<kern::ScoreTask>());
+    const size_t nt = BuildTasks(nunit, next->cand_begin, next->n, next->q_first, next->q_end, counts, offsets,
+                                 per_block, nqmax, per_block / 4, hs.as<kern::ScoreTask>());
     I.task_buf[nb].Reserve(nt * sizeof(kern::ScoreTask));
     HIP_CHECK(hipMemcpyAsync(I.task_buf[nb].p, hs.p, nt * sizeof(kern::ScoreTask), hipMemcpyHostToDevice,
                              S(copy_stream_)));
@@ -1065,7 +1162,8 @@ void DeviceModule::ScoreFinish() {
     HIP_CHECK(hipMemcpy(list.data(), I.guard_list.p, list.size() * 4, hipMemcpyDeviceToHost));
     std::vector<kern::ScoreTask> redo(nguard);
     for (uint32_t k = 0; k < nguard; ++k)
-      redo[k] = kern::ScoreTask{P.cand_begin + list[2 * k], 1u, list[2 * k + 1], 1u, 0u};
+      redo[k] = kern::ScoreTask{P.cand_begin + list[2 * k], 1u, list[2 * k + 1], 1u, 1u,
+                                P.cand_begin + list[2 * k] + 1, list[2 * k + 1] + 1, 0u};
     I.tasks_redo.Reserve(redo.size() * sizeof(kern::ScoreTask));
     HIP_CHECK(hipMemcpy(I.tasks_redo.p, redo.data(), redo.size() * sizeof(kern::ScoreTask), hipMemcpyHostToDevice));
     kern::ScoreArgs r = P.args;

@@ -842,6 +842,13 @@ struct ScoreTask {
   uint32_t count;            // candidates in this task
   uint32_t q_first;          // first query of the task (profile slot 0)
   uint32_t q_count;          // profile slots used
+  // k_score16f UNIT (paired tasks, BuildScoreTasksPaired): candidates
+  // [begin, begin + count1) of query q_first (slot 0), then [begin2, begin2 +
+  // count - count1) of query q_second (slot 1); the other kernels take
+  // [begin, begin + count) over the consecutive queries q_first.. instead
+  uint32_t count1;
+  unsigned long long begin2;
+  uint32_t q_second;
   uint32_t pad;
 };
 
@@ -1212,7 +1219,8 @@ __device__ __forceinline__ void BuildProfileUnit(const ScoreArgs &a, const Score
 #pragma unroll
       for (int c = 0; c < 32; ++c) dst[c * RS] = drop | 0x10000u;
     } else {
-      const uint32_t q = a.qseq[(size_t)(t.q_first + slot) * a.L + (r - a.pad)];
+      const uint32_t query = slot ? t.q_second : t.q_first;  // paired task: two ranges
+      const uint32_t q = a.qseq[(size_t)query * a.L + (r - a.pad)];
       const uint4 *src = reinterpret_cast<const uint4 *>(s_enc + q * 32);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -1471,17 +1479,26 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
   const bool vB = in_group && 2 * pair + 1 < t.count;
   // a wave past the task's last candidate has nothing to do (no barrier follows)
   if (!__builtin_amdgcn_ballot_w64(vA)) return;
-  const unsigned long long cA = t.begin + 2 * pair, cB = cA + 1;
+  unsigned long long cA = t.begin + 2 * pair, cB = cA + 1;
   uint32_t slotA = 0, slotB = 0, offA = 0, offB = 0, wA = 0, wB = 0;
+  if constexpr (UNIT) {
+    // paired task: local index l < count1 is query q_first's (slot 0), the
+    // rest query q_second's (slot 1)
+    const uint32_t lA = 2 * pair, lB = lA + 1;
+    slotA = lA >= t.count1;
+    slotB = lB >= t.count1;
+    cA = slotA ? t.begin2 + (lA - t.count1) : t.begin + lA;
+    cB = slotB ? t.begin2 + (lB - t.count1) : t.begin + lB;
+  }
   if (vA) {
-    slotA = a.cand_qid[cA] - t.q_first;
+    if constexpr (!UNIT) slotA = a.cand_qid[cA] - t.q_first;
     int o = (int)(a.cand_start[cA] - a.extend);
     offA = o < 0 ? 0u : (uint32_t)o;
     wA = a.base;
     if (offA + wA > a.dblen) wA = a.dblen - offA;
   }
   if (vB) {
-    slotB = a.cand_qid[cB] - t.q_first;
+    if constexpr (!UNIT) slotB = a.cand_qid[cB] - t.q_first;
     int o = (int)(a.cand_start[cB] - a.extend);
     offB = o < 0 ? 0u : (uint32_t)o;
     wB = a.base;
@@ -2666,6 +2683,10 @@ __global__ __launch_bounds__(256) void k_tb_pairs(const uint32_t *qid, const uin
       e[at] = v;
     }
     uint32_t items = 0;
+    // the histogram: most items of a run share their key (full windows), so
+    // equal consecutive keys are added at once (one LDS atomic per key change:
+    // same-address atomics of the lanes serialise in the LDS)
+    uint32_t run_key = 0xFFFFFFFFu, run_n = 0;
     for (uint32_t k = 0; k < m;) {
       const uint32_t a = first + (uint32_t)(e[k] & 0xFFFFu), wa = (uint32_t)(e[k] >> 16) & 0xFFFFu;
       uint32_t b = 0xFFFFFFFFu, wb = 0;
@@ -2681,8 +2702,14 @@ __global__ __launch_bounds__(256) void k_tb_pairs(const uint32_t *qid, const uin
       pair_b[first + items] = b;
       key[first + items] = kk;
       ++items;
-      atomicAdd(&s_hist[kk], 1u);
+      if (kk != run_key) {
+        if (run_n) atomicAdd(&s_hist[run_key], run_n);
+        run_key = kk;
+        run_n = 0;
+      }
+      ++run_n;
     }
+    if (run_n) atomicAdd(&s_hist[run_key], run_n);
     for (uint32_t k = items; k < len; ++k) key[first + k] = 0;
     if (items) atomicAdd(&s_total, items);
   }

@@ -394,6 +394,8 @@ class Search {
       if (cnt > thr) Emit(i, bin << o_.log_region, &count);
       if (count > o_.max_list) {  // the query stays carried into the next batch
         next_query_ = i + 1;
+        // test hook: where the batch loop cuts (query i's candidates open the next batch)
+        if (getenv("GHOSTM_ORACLE_BATCHES")) fprintf(stderr, "batch_cut %u\n", i);
         return;
       }
       batch->insert(batch->end(), carry_.begin(), carry_.end());

@@ -43,15 +43,17 @@ def test_gpu_matches_reference_golden(ds, var, opts, env, dataset, golden, tmp_p
     assert cases.sha256(str(tmp_path / "g.out")) == want["sha256"]
 
 
+@pytest.mark.parametrize("tasks", ["paired", "consecutive"])
 @pytest.mark.parametrize("ds,var,opts,env", cases.VARIANTS, ids=[f"{v[0]}/{v[1]}" for v in cases.VARIANTS])
-def test_gpu_unit_k2_matches_reference_golden(ds, var, opts, env, dataset, golden, tmp_path):
+def test_gpu_unit_k2_matches_reference_golden(ds, var, opts, env, tasks, dataset, golden, tmp_path):
     """Every golden variant with K2's unit-pair kernel forced (GHOSTM_K2=unit;
-    by default it runs only on segments averaging >= 80 candidates per query):
-    windows crossing one or several subject ENDs (the testset's short
-    subjects), a window whose first column is END, the DB's end, one-subject
-    DBs, short queries (S = 16 and 8) and every gap setting."""
+    by default it runs only on segments averaging enough candidates per
+    query), with its tasks as query pairs (two candidate ranges per block) or
+    as consecutive runs: windows crossing one or several subject ENDs (the
+    testset's short subjects), a window whose first column is END, the DB's
+    end, one-subject DBs, short queries (S = 16 and 8) and every gap setting."""
     d = dataset(ds)
-    text, st = _gpu_text(d, opts, dict(env, GHOSTM_K2="unit"), str(tmp_path / "g.out"))
+    text, st = _gpu_text(d, opts, dict(env, GHOSTM_K2="unit", GHOSTM_K2_TASKS=tasks), str(tmp_path / "g.out"))
     want = golden["aln"][f"{ds}/{var}"]
     (tmp_path / "g.out").write_bytes(text)
     assert cases.sha256(str(tmp_path / "g.out")) == want["sha256"]
