@@ -2915,6 +2915,18 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
         qoff[1] = v.y;
       }
     }
+    // SWAR: every row's table byte offset in a register of its own, so a row's
+    // table address is one full-rate v_add_u32 (the packed bytes took one SDWA
+    // add per row, an instruction of the half-rate class); 24 more VGPRs, still
+    // three waves per SIMD
+    uint32_t qrow[SWAR ? S : 1];
+    if constexpr (SWAR) {
+#pragma unroll
+      for (int u = 0; u < S; ++u) {
+        qrow[u] = (qoff[u >> 2] >> (8 * (u & 3))) & 0xFFu;
+        asm volatile("" : "+v"(qrow[u]));  // kept: else the extract folds back into an SDWA add per row
+      }
+    }
     uint32_t H[S], E[S];
     // FRAMED: sigma(j) = (G + j) * ext_pen, this lane starts at column -i
     const uint32_t EXTP = SWAR ? (uint32_t)extp * 0x10001u : Cells<true>::Pair(extp);
@@ -2991,7 +3003,10 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
       const hf2 Z1 = SWAR ? HF(sig + EXTP) : HF(W(HF(sig) + HF(EXTP)));  // FRAMED: the next column's frame
       const hf2 KOE = HF(Cells<true>::Pair(a.open - a.ext)), NEXT = HF(Cells<true>::Pair(a.ext));
       const char *tp = reinterpret_cast<const char *>(s_pair) + cbase;
-      auto T = [&](int u) { return *reinterpret_cast<const uint32_t *>(tp + ((qoff[u >> 2] >> (8 * (u & 3))) & 0xFFu)); };
+      auto T = [&](int u) {
+        if constexpr (SWAR) return *reinterpret_cast<const uint32_t *>(tp + qrow[u]);
+        else return *reinterpret_cast<const uint32_t *>(tp + ((qoff[u >> 2] >> (8 * (u & 3))) & 0xFFu));
+      };
       uint32_t diag = diag0, F = fin, cm = sig;
       if constexpr (FRAMED) {
         // software-pipelined by chunks of eight rows: the next chunk's eight
@@ -2999,16 +3014,19 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
         // diagonal sum is formed one row ahead, from the old H just before the
         // row above overwrites it
         constexpr int CH = 8;
-        uint32_t t[CH], tn[CH];
+        // two read-ahead sets used in turn by chunk parity (a fixed register
+        // set per chunk after unrolling: no copies of the next chunk's reads)
+        uint32_t tt[2][CH];
 #pragma unroll
-        for (int u = 0; u < CH; ++u) t[u] = T(u);
+        for (int u = 0; u < CH; ++u) tt[0][u] = T(u);
         auto dsum = [](uint32_t h, uint32_t tv) -> uint32_t {
           if constexpr (SWAR) return h + tv;  // v_add_u32 over both halves
           else return W(HF(h) + HF(tv));
         };
-        uint32_t sc = dsum(diag, t[0]);
+        uint32_t sc = dsum(diag, tt[0][0]);
 #pragma unroll
         for (int k = 0; k < S; k += CH) {
+          uint32_t *t = tt[(k / CH) & 1], *tn = tt[((k / CH) & 1) ^ 1];
           if (k + CH < S) {
 #pragma unroll
             for (int u = 0; u < CH; ++u) tn[u] = T(k + CH + u);
@@ -3031,10 +3049,6 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
                          C::Max3(H[k + 6], H[k + 7], cm));
           else
             cm = C::Max3(C::Max3(H[k], H[k + 1], H[k + 2]), H[k + 3], cm);
-          if (k + CH < S) {
-#pragma unroll
-            for (int u = 0; u < CH; ++u) t[u] = tn[u];
-          }
           __builtin_amdgcn_sched_barrier(0);
         }
       } else {
