@@ -16,6 +16,7 @@
 #include "device.h"
 #include "formats.h"
 #include "kernels.h"
+#include "score_tasks.h"
 
 namespace ghostm {
 
@@ -130,7 +131,8 @@ struct DeviceModule::Impl {
   struct Prepared {
     bool valid = false;
     uint64_t cand_begin = 0, n = 0;
-    uint32_t count = 0, per_block = 0, qmax = 0;
+    uint32_t count = 0, per_block = 0;
+    bool swar = false, unit = false;  // the encoding they were built for; the kernel they chose
     int buf = 0;
   } prepared;
   struct ScoreState {                       // the launched, not yet finished K2
@@ -789,156 +791,6 @@ void DeviceModule::CopyStarts(uint64_t begin, uint64_t n, uint32_t *out) {
   SettleSeedTime();
 }
 
-// K2 tasks: runs of <= per_block consecutive candidates spanning <= Qmax queries,
-// written straight into page-locked staging (no fresh host vector per segment:
-// its first touch cost more than the loop). A task closes when full, when it
-// spans Qmax queries, or at the end, so ScoreTaskBound is an upper bound.
-static size_t ScoreTaskBound(uint64_t n, uint32_t q_first, uint32_t q_end, uint32_t per_block, uint32_t qmax) {
-  // paired unit tasks: full blocks plus at most one remainder task per query
-  return (size_t)(n / per_block) + (q_end - q_first) + 2;
-}
-static size_t BuildScoreTasks(uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32_t q_end,
-                              const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets,
-                              uint32_t per_block, uint32_t qmax, kern::ScoreTask *out) {
-  size_t nt = 0;
-  kern::ScoreTask cur{};
-  bool open_task = false;
-  auto flush = [&]() {
-    if (open_task && cur.count) out[nt++] = cur;
-    open_task = false;
-  };
-  const uint64_t cand_end = cand_begin + n;
-  for (uint32_t qi = q_first; qi < q_end; ++qi) {
-    uint64_t lo = std::max<uint64_t>(offsets[qi], cand_begin);
-    const uint64_t hi = std::min<uint64_t>(offsets[qi] + counts[qi], cand_end);
-    while (lo < hi) {
-      if (open_task && (cur.count == per_block || qi - cur.q_first >= qmax)) flush();
-      if (!open_task) {
-        cur = kern::ScoreTask{};
-        cur.begin = lo;
-        cur.q_first = qi;
-        open_task = true;
-      }
-      const uint64_t take = std::min<uint64_t>(hi - lo, per_block - cur.count);
-      cur.count += (uint32_t)take;
-      cur.q_count = qi - cur.q_first + 1;
-      cur.count1 = cur.count;
-      cur.begin2 = cur.begin + cur.count;
-      cur.q_second = cur.q_first + 1;
-      lo += take;
-    }
-  }
-  flush();
-  return nt;
-}
-
-// Tasks of k_score16f's unit-pair kernel (two query profiles per block): each
-// query's candidates in full blocks of per_block, and the remainders paired two
-// queries to a block, so that the pair fills fewer waves than the two alone
-// would. A wave (64 lanes, `wave_slots` candidates) costs the same however few
-// of its candidates are real, so a remainder of r costs ceil(r / wave_slots)
-// waves; two remainders whose partial waves fit one wave together save one.
-// Each remainder takes the largest partner that saves a wave (best fit by the
-// partial wave's size), else runs alone. At 63 candidates per query (cfg 3)
-// consecutive pairs of queries left 8 % more waves than four queries per block.
-static size_t BuildScoreTasksPaired(uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32_t q_end,
-                                    const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets,
-                                    uint32_t per_block, uint32_t wave_slots, kern::ScoreTask *out) {
-  size_t nt = 0;
-  auto single = [&](uint32_t q, uint64_t begin, uint32_t count) {
-    kern::ScoreTask t{};
-    t.begin = begin;
-    t.count = count;
-    t.count1 = count;
-    t.q_first = q;
-    t.q_count = 1;
-    t.begin2 = begin + count;
-    t.q_second = q;
-    out[nt++] = t;
-  };
-  // remainders by size (1 .. per_block - 1): stacks of (query, first candidate)
-  std::vector<std::vector<std::pair<uint32_t, uint64_t>>> rem(per_block);
-  const uint64_t cand_end = cand_begin + n;
-  for (uint32_t qi = q_first; qi < q_end; ++qi) {
-    uint64_t lo = std::max<uint64_t>(offsets[qi], cand_begin);
-    const uint64_t hi = std::min<uint64_t>(offsets[qi] + counts[qi], cand_end);
-    if (lo >= hi) continue;
-    while (hi - lo >= per_block) {
-      single(qi, lo, per_block);
-      lo += per_block;
-    }
-    if (hi > lo) rem[hi - lo].emplace_back(qi, lo);
-  }
-  auto partial = [&](uint32_t r) { return r - (r - 1) / wave_slots * wave_slots; };  // 1 .. wave_slots
-  for (uint32_t r1 = per_block - 1; r1 >= 1; --r1) {
-    while (!rem[r1].empty()) {
-      const std::pair<uint32_t, uint64_t> a = rem[r1].back();
-      rem[r1].pop_back();
-      // the partner with the largest partial wave that still fits beside r1's
-      const uint32_t room = wave_slots - partial(r1);
-      uint32_t pick = 0;
-      for (uint32_t p = room; p >= 1 && !pick; --p)
-        for (uint32_t r2 = p; r2 <= r1 && r1 + r2 <= per_block; r2 += wave_slots)
-          if (!rem[r2].empty()) pick = r2;  // the largest with this partial wave
-      if (!pick) {
-        single(a.first, a.second, r1);
-        continue;
-      }
-      const std::pair<uint32_t, uint64_t> b = rem[pick].back();
-      rem[pick].pop_back();
-      kern::ScoreTask t{};
-      t.begin = a.second;
-      t.count1 = r1;
-      t.q_first = a.first;
-      t.begin2 = b.second;
-      t.q_second = b.first;
-      t.count = r1 + pick;
-      t.q_count = 2;
-      out[nt++] = t;
-    }
-  }
-  return nt;
-}
-
-// The unit kernel takes whichever of the paired and the consecutive tasks
-// fill fewer waves (consecutive runs win narrowly near 127 candidates per
-// query, pairs clearly at 63); GHOSTM_K2_TASKS=paired|consecutive forces one.
-static size_t BuildTasks(bool unit, uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32_t q_end,
-                         const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets,
-                         uint32_t per_block, uint32_t qmax, uint32_t wave_slots, kern::ScoreTask *out) {
-  if (!unit) return BuildScoreTasks(cand_begin, n, q_first, q_end, counts, offsets, per_block, qmax, out);
-  const char *force = getenv("GHOSTM_K2_TASKS");
-  if (force && strcmp(force, "consecutive") == 0)
-    return BuildScoreTasks(cand_begin, n, q_first, q_end, counts, offsets, per_block, qmax, out);
-  const size_t np = BuildScoreTasksPaired(cand_begin, n, q_first, q_end, counts, offsets, per_block, wave_slots, out);
-  if (force && strcmp(force, "paired") == 0) return np;
-  auto waves = [&](const kern::ScoreTask *t, size_t nt) {
-    uint64_t w = 0;
-    for (size_t k = 0; k < nt; ++k) w += (t[k].count + wave_slots - 1) / wave_slots;
-    return w;
-  };
-  std::vector<kern::ScoreTask> consecutive(ScoreTaskBound(n, q_first, q_end, per_block, qmax));
-  const size_t nc = BuildScoreTasks(cand_begin, n, q_first, q_end, counts, offsets, per_block, qmax,
-                                    consecutive.data());
-  if (waves(consecutive.data(), nc) >= waves(out, np)) return np;
-  std::copy(consecutive.begin(), consecutive.begin() + nc, out);
-  return nc;
-}
-
-// k_score16f's unit-pair kernel (UNIT) holds the profiles of kScoreQmaxUnit
-// queries per block instead of kScoreQmax: used where a segment averages at
-// least 80 candidates per query, so that two queries still fill a block's 128
-// candidate slots (a simulation with Poisson counts: 8 % more non-empty waves
-// than with 4 queries per block at 63 per query, 5.6 % at 80, 0.3 % at 127;
-// cfg 4 averages 127, cfg 3 63). GHOSTM_K2=unit forces it, swar16 keeps the
-// 16-bit profile kernel.
-static bool ScoreUnit(bool swar, uint64_t n, uint32_t q_first, uint32_t q_end) {
-  if (!swar) return false;
-  const char *force = getenv("GHOSTM_K2");
-  if (force && strcmp(force, "unit") == 0) return true;
-  if (force && strcmp(force, "swar16") == 0) return false;
-  return q_end > q_first && n >= (uint64_t)80 * (q_end - q_first);
-}
 
 // the packed K2 encodings (two candidates per lane) whenever every value fits
 static bool ScorePacked(const int *h_matrix, uint32_t L, uint32_t base, const GapConfig &gap) {
@@ -999,16 +851,18 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
   int guard = swar ? 0 : framed ? (bound + sigma_max < 2040 ? 0 : (int)(2040 - sigma_max)) : (bound < 2048 ? 0 : 2000);
   if (half && getenv("GHOSTM_K2_GUARD")) guard = atoi(getenv("GHOSTM_K2_GUARD"));  // tests: force re-scores
   const uint32_t per_block = ScorePerBlock(q, base, gap);
-  const bool unit = ScoreUnit(swar, n, q_first, q_end);
-  const uint32_t qmax = unit ? kern::kScoreQmaxUnit : kern::kScoreQmax;
-  // tasks: prepared for this range by the previous launch (uploaded on the copy
-  // stream into the other task buffer), else built and uploaded here
+  // tasks, and with them the kernel (score_tasks.h BuildTasks: the unit-pair
+  // kernel where its blocks are not too many more): prepared for this range by
+  // the previous launch (uploaded on the copy stream into the other task
+  // buffer), else built and uploaded here
+  bool unit = false;
   int buf = -1;
   size_t ntasks = 0;
   if (I.prepared.valid && I.prepared.cand_begin == cand_begin && I.prepared.n == n &&
-      I.prepared.per_block == per_block && I.prepared.qmax == qmax) {
+      I.prepared.per_block == per_block && I.prepared.swar == swar) {
     buf = I.prepared.buf;
     ntasks = I.prepared.count;
+    unit = I.prepared.unit;
     HIP_CHECK(hipStreamWaitEvent(S(stream_), I.ev_tasks, 0));
   }
   const bool stale = I.prepared.valid;  // an upload nothing will use may still read its staging
@@ -1019,10 +873,20 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
     // page-locked staging per task buffer: this one's last upload was read by
     // a launch that has been waited for, so the copy needs no wait either
     PinnedBuf &hs = I.h_tasks[buf];
-    hs.Reserve(ScoreTaskBound(n, q_first, q_end, per_block, qmax) * sizeof(kern::ScoreTask));
-    ntasks = BuildTasks(unit, cand_begin, n, q_first, q_end, counts, offsets, per_block, qmax, per_block / 4,
-                        hs.as<kern::ScoreTask>());
+    hs.Reserve(ScoreTaskBound(n, q_first, q_end, per_block, kern::kScoreQmaxUnit) * sizeof(kern::ScoreTask));
+    ntasks = BuildTasks(swar, cand_begin, n, q_first, q_end, counts, offsets, per_block, hs.as<kern::ScoreTask>(),
+                        &unit);
     TraceMark("tasks", ntasks);
+    if (const char *dump = getenv("GHOSTM_DEBUG_TASKS")) {  // diagnostics: the launch's tasks and counts
+      if (FILE *f = fopen(dump, "ab")) {
+        const uint64_t hdr[6] = {cand_begin, n, q_first, q_end, (uint64_t)unit, (uint64_t)ntasks};
+        fwrite(hdr, 8, 6, f);
+        fwrite(hs.p, sizeof(kern::ScoreTask), ntasks, f);
+        fwrite(counts.data() + q_first, 4, q_end - q_first, f);
+        fwrite(offsets.data() + q_first, 8, q_end - q_first, f);
+        fclose(f);
+      }
+    }
     const size_t tb = ntasks * sizeof(kern::ScoreTask);
     I.task_buf[buf].Reserve(tb);
     HIP_CHECK(hipMemcpyAsync(I.task_buf[buf].p, hs.p, tb, hipMemcpyHostToDevice, S(stream_)));
@@ -1122,16 +986,16 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
   if (next && next->n) {
     const int nb = I.task_turn;
     PinnedBuf &hs = I.h_tasks[nb];
-    const bool nunit = ScoreUnit(swar, next->n, next->q_first, next->q_end);
-    const uint32_t nqmax = nunit ? kern::kScoreQmaxUnit : kern::kScoreQmax;
-    hs.Reserve(ScoreTaskBound(next->n, next->q_first, next->q_end, per_block, nqmax) * sizeof(kern::ScoreTask));
-    const size_t nt = BuildTasks(nunit, next->cand_begin, next->n, next->q_first, next->q_end, counts, offsets,
-                                 per_block, nqmax, per_block / 4, hs.as<kern::ScoreTask>());
+    bool nunit = false;
+    hs.Reserve(ScoreTaskBound(next->n, next->q_first, next->q_end, per_block, kern::kScoreQmaxUnit) *
+               sizeof(kern::ScoreTask));
+    const size_t nt = BuildTasks(swar, next->cand_begin, next->n, next->q_first, next->q_end, counts, offsets,
+                                 per_block, hs.as<kern::ScoreTask>(), &nunit);
     I.task_buf[nb].Reserve(nt * sizeof(kern::ScoreTask));
     HIP_CHECK(hipMemcpyAsync(I.task_buf[nb].p, hs.p, nt * sizeof(kern::ScoreTask), hipMemcpyHostToDevice,
                              S(copy_stream_)));
     HIP_CHECK(hipEventRecord(I.ev_tasks, S(copy_stream_)));
-    I.prepared = Impl::Prepared{true, next->cand_begin, next->n, (uint32_t)nt, per_block, nqmax, nb};
+    I.prepared = Impl::Prepared{true, next->cand_begin, next->n, (uint32_t)nt, per_block, swar, nunit, nb};
   }
 }
 

@@ -25,6 +25,7 @@
 #include <type_traits>
 
 #include "libstdcxx_sort.h"
+#include "score_task.h"
 
 namespace ghostm {
 namespace kern {
@@ -830,27 +831,11 @@ __device__ inline void WaveAddCells(unsigned long long *counter, unsigned long l
 
 // ------------------------------------------------------------------ K2 score
 constexpr int kScoreBlock = 256;
-constexpr int kScoreQmax = 4;
-constexpr int kScoreQmaxUnit = 2;  // k_score16f UNIT: 32-bit profile words, half the queries per block
 constexpr uint32_t kProfRows = 26;
 constexpr uint32_t kProfRows16 = 32;  // packed kernels: one profile row per residue code
 constexpr uint32_t kFillCode = 26;     // k_score16f: profile row of the columns before the window
 constexpr uint32_t kDbFrontPad = 64;  // END bytes in front of the DB residues (device.hip)
 
-struct ScoreTask {
-  unsigned long long begin;  // first candidate (global index)
-  uint32_t count;            // candidates in this task
-  uint32_t q_first;          // first query of the task (profile slot 0)
-  uint32_t q_count;          // profile slots used
-  // k_score16f UNIT (paired tasks, BuildScoreTasksPaired): candidates
-  // [begin, begin + count1) of query q_first (slot 0), then [begin2, begin2 +
-  // count - count1) of query q_second (slot 1); the other kernels take
-  // [begin, begin + count) over the consecutive queries q_first.. instead
-  uint32_t count1;
-  unsigned long long begin2;
-  uint32_t q_second;
-  uint32_t pad;
-};
 
 struct ScoreArgs {
   const uint8_t *qseq;
@@ -1483,10 +1468,13 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
   uint32_t slotA = 0, slotB = 0, offA = 0, offB = 0, wA = 0, wB = 0;
   if constexpr (UNIT) {
     // paired task: local index l < count1 is query q_first's (slot 0), the
-    // rest query q_second's (slot 1)
+    // rest query q_second's (slot 1). A half past the task's candidates reads
+    // slot 0, which every task builds: the other half's diagonal sum takes the
+    // constant 1 from this half's profile word (PkMadUnit), so it must be a
+    // built unit word, never a stale slot-1 row
     const uint32_t lA = 2 * pair, lB = lA + 1;
-    slotA = lA >= t.count1;
-    slotB = lB >= t.count1;
+    slotA = vA && lA >= t.count1;
+    slotB = vB && lB >= t.count1;
     cA = slotA ? t.begin2 + (lA - t.count1) : t.begin + lA;
     cB = slotB ? t.begin2 + (lB - t.count1) : t.begin + lB;
   }
@@ -1782,12 +1770,12 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
       if (vA && BA >= a.guard) {
         const uint32_t k = atomicAdd(a.guard_count, 1u);
         a.guard_list[2 * k] = (uint32_t)(cA - a.out_base);
-        a.guard_list[2 * k + 1] = t.q_first + slotA;
+        a.guard_list[2 * k + 1] = UNIT ? (slotA ? t.q_second : t.q_first) : t.q_first + slotA;
       }
       if (vB && BB >= a.guard) {
         const uint32_t k = atomicAdd(a.guard_count, 1u);
         a.guard_list[2 * k] = (uint32_t)(cB - a.out_base);
-        a.guard_list[2 * k + 1] = t.q_first + slotB;
+        a.guard_list[2 * k + 1] = UNIT ? (slotB ? t.q_second : t.q_first) : t.q_first + slotB;
       }
     }
   }
@@ -2915,18 +2903,6 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
         qoff[1] = v.y;
       }
     }
-    // SWAR: every row's table byte offset in a register of its own, so a row's
-    // table address is one full-rate v_add_u32 (the packed bytes took one SDWA
-    // add per row, an instruction of the half-rate class); 24 more VGPRs, still
-    // three waves per SIMD
-    uint32_t qrow[SWAR ? S : 1];
-    if constexpr (SWAR) {
-#pragma unroll
-      for (int u = 0; u < S; ++u) {
-        qrow[u] = (qoff[u >> 2] >> (8 * (u & 3))) & 0xFFu;
-        asm volatile("" : "+v"(qrow[u]));  // kept: else the extract folds back into an SDWA add per row
-      }
-    }
     uint32_t H[S], E[S];
     // FRAMED: sigma(j) = (G + j) * ext_pen, this lane starts at column -i
     const uint32_t EXTP = SWAR ? (uint32_t)extp * 0x10001u : Cells<true>::Pair(extp);
@@ -3003,10 +2979,7 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
       const hf2 Z1 = SWAR ? HF(sig + EXTP) : HF(W(HF(sig) + HF(EXTP)));  // FRAMED: the next column's frame
       const hf2 KOE = HF(Cells<true>::Pair(a.open - a.ext)), NEXT = HF(Cells<true>::Pair(a.ext));
       const char *tp = reinterpret_cast<const char *>(s_pair) + cbase;
-      auto T = [&](int u) {
-        if constexpr (SWAR) return *reinterpret_cast<const uint32_t *>(tp + qrow[u]);
-        else return *reinterpret_cast<const uint32_t *>(tp + ((qoff[u >> 2] >> (8 * (u & 3))) & 0xFFu));
-      };
+      auto T = [&](int u) { return *reinterpret_cast<const uint32_t *>(tp + ((qoff[u >> 2] >> (8 * (u & 3))) & 0xFFu)); };
       uint32_t diag = diag0, F = fin, cm = sig;
       if constexpr (FRAMED) {
         // software-pipelined by chunks of eight rows: the next chunk's eight

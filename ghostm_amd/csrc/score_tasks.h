@@ -1,0 +1,235 @@
+// score_tasks.h — K2 task lists (host only; included by device.hip, unit-tested
+// with g++ by tests/native/test_score_tasks.cpp). A task is one workgroup of
+// k_score*: up to per_block candidates and the profiles of the queries they
+// belong to.
+#pragma once
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <utility>
+#include <vector>
+
+#include "score_task.h"
+
+
+namespace ghostm {
+
+// K2 tasks: runs of <= per_block consecutive candidates spanning <= Qmax queries,
+// written straight into page-locked staging (no fresh host vector per segment:
+// its first touch cost more than the loop). A task closes when full, when it
+// spans Qmax queries, or at the end, so ScoreTaskBound is an upper bound.
+inline size_t ScoreTaskBound(uint64_t n, uint32_t q_first, uint32_t q_end, uint32_t per_block, uint32_t qmax) {
+  // paired unit tasks: full blocks plus at most one remainder task per query
+  return (size_t)(n / per_block) + (q_end - q_first) + 2;
+}
+inline size_t BuildScoreTasks(uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32_t q_end,
+                              const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets,
+                              uint32_t per_block, uint32_t qmax, kern::ScoreTask *out) {
+  size_t nt = 0;
+  kern::ScoreTask cur{};
+  bool open_task = false;
+  auto flush = [&]() {
+    if (open_task && cur.count) out[nt++] = cur;
+    open_task = false;
+  };
+  const uint64_t cand_end = cand_begin + n;
+  for (uint32_t qi = q_first; qi < q_end; ++qi) {
+    uint64_t lo = std::max<uint64_t>(offsets[qi], cand_begin);
+    const uint64_t hi = std::min<uint64_t>(offsets[qi] + counts[qi], cand_end);
+    while (lo < hi) {
+      if (open_task && (cur.count == per_block || qi - cur.q_first >= qmax)) flush();
+      if (!open_task) {
+        cur = kern::ScoreTask{};
+        cur.begin = lo;
+        cur.q_first = qi;
+        open_task = true;
+      }
+      const uint64_t take = std::min<uint64_t>(hi - lo, per_block - cur.count);
+      cur.count += (uint32_t)take;
+      cur.q_count = qi - cur.q_first + 1;
+      // the unit kernel reads a task as two ranges: the first query's
+      // candidates, then (contiguous here) the second query's
+      if (qi == cur.q_first) cur.count1 += (uint32_t)take;
+      cur.begin2 = cur.begin + cur.count1;
+      cur.q_second = cur.q_first + 1;
+      lo += take;
+    }
+  }
+  flush();
+  return nt;
+}
+
+// Tasks of k_score16f's unit-pair kernel (two query profiles per block): each
+// query's candidates in full blocks of per_block, and the remainders paired two
+// queries to a block, best fit: each remainder (largest first) takes the
+// largest remainder that still fits beside it. A block holds its LDS rows for
+// a whole wave-duration however few of its waves are live (the LDS, not the
+// waves, limits the unit kernel to four blocks per CU), so what counts is the
+// number of blocks. At 63 candidates per query (cfg 3) consecutive runs of two
+// queries make 17 % more blocks than the pairs (Poisson counts: 58.4 K against
+// 50.0 K per 100 K queries); from ~80 per query on they win instead (pairs of
+// remainders above 64 cannot share a block, consecutive runs split queries).
+inline size_t BuildScoreTasksPaired(uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32_t q_end,
+                                    const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets,
+                                    uint32_t per_block, kern::ScoreTask *out) {
+  size_t nt = 0;
+  auto single = [&](uint32_t q, uint64_t begin, uint32_t count) {
+    kern::ScoreTask t{};
+    t.begin = begin;
+    t.count = count;
+    t.count1 = count;
+    t.q_first = q;
+    t.q_count = 1;
+    t.begin2 = begin + count;
+    t.q_second = q;
+    out[nt++] = t;
+  };
+  // remainders by size (1 .. per_block - 1): stacks of (query, first candidate)
+  std::vector<std::vector<std::pair<uint32_t, uint64_t>>> rem(per_block);
+  const uint64_t cand_end = cand_begin + n;
+  for (uint32_t qi = q_first; qi < q_end; ++qi) {
+    uint64_t lo = std::max<uint64_t>(offsets[qi], cand_begin);
+    const uint64_t hi = std::min<uint64_t>(offsets[qi] + counts[qi], cand_end);
+    if (lo >= hi) continue;
+    while (hi - lo >= per_block) {
+      single(qi, lo, per_block);
+      lo += per_block;
+    }
+    if (hi > lo) rem[hi - lo].emplace_back(qi, lo);
+  }
+  for (uint32_t r1 = per_block - 1; r1 >= 1; --r1) {
+    while (!rem[r1].empty()) {
+      const std::pair<uint32_t, uint64_t> a = rem[r1].back();
+      rem[r1].pop_back();
+      uint32_t pick = 0;
+      for (uint32_t r2 = std::min(r1, per_block - r1); r2 >= 1 && !pick; --r2)
+        if (!rem[r2].empty()) pick = r2;
+      if (!pick) {
+        single(a.first, a.second, r1);
+        continue;
+      }
+      const std::pair<uint32_t, uint64_t> b = rem[pick].back();
+      rem[pick].pop_back();
+      kern::ScoreTask t{};
+      t.begin = a.second;
+      t.count1 = r1;
+      t.q_first = a.first;
+      t.begin2 = b.second;
+      t.q_second = b.first;
+      t.count = r1 + pick;
+      t.q_count = 2;
+      out[nt++] = t;
+    }
+  }
+  return nt;
+}
+
+// Consecutive runs of at most qmax queries without building them: the blocks
+// the 16-bit-row kernel (four query profiles per block) would launch.
+inline size_t CountScoreTasks(uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32_t q_end,
+                              const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets,
+                              uint32_t per_block, uint32_t qmax) {
+  size_t nt = 0;
+  uint32_t cur = 0, open_q = 0;
+  bool open_task = false;
+  const uint64_t cand_end = cand_begin + n;
+  for (uint32_t qi = q_first; qi < q_end; ++qi) {
+    uint64_t lo = std::max<uint64_t>(offsets[qi], cand_begin);
+    const uint64_t hi = std::min<uint64_t>(offsets[qi] + counts[qi], cand_end);
+    while (lo < hi) {
+      if (open_task && (cur == per_block || qi - open_q >= qmax)) {
+        ++nt;
+        open_task = false;
+      }
+      if (!open_task) {
+        cur = 0;
+        open_q = qi;
+        open_task = true;
+      }
+      const uint64_t take = std::min<uint64_t>(hi - lo, per_block - cur);
+      cur += (uint32_t)take;
+      lo += take;
+    }
+  }
+  return nt + (open_task && cur ? 1 : 0);
+}
+
+// The blocks BuildScoreTasksPaired would make, from a histogram of the
+// remainders (no tasks built).
+inline size_t CountPairedTasks(uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32_t q_end,
+                               const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets,
+                               uint32_t per_block) {
+  std::vector<uint64_t> rem(per_block, 0);
+  size_t nt = 0;
+  const uint64_t cand_end = cand_begin + n;
+  for (uint32_t qi = q_first; qi < q_end; ++qi) {
+    const uint64_t lo = std::max<uint64_t>(offsets[qi], cand_begin);
+    const uint64_t hi = std::min<uint64_t>(offsets[qi] + counts[qi], cand_end);
+    if (lo >= hi) continue;
+    nt += (hi - lo) / per_block;
+    ++rem[(hi - lo) % per_block];
+  }
+  rem[0] = 0;
+  // BuildScoreTasksPaired's greedy in batches: every remainder of size r1 takes
+  // the same partner size while partners of that size last
+  for (uint32_t r1 = per_block - 1; r1 >= 1; --r1) {
+    while (rem[r1]) {
+      uint32_t r2 = std::min(r1, per_block - r1);
+      while (r2 >= 1 && !(r2 == r1 ? rem[r1] >= 2 : rem[r2] >= 1)) --r2;
+      if (r2 == 0) {
+        nt += rem[r1];  // no partner fits: singles
+        rem[r1] = 0;
+      } else if (r2 == r1) {
+        const uint64_t k = rem[r1] / 2;
+        nt += k;
+        rem[r1] -= 2 * k;
+      } else {
+        const uint64_t k = std::min(rem[r1], rem[r2]);
+        nt += k;
+        rem[r1] -= k;
+        rem[r2] -= k;
+      }
+    }
+  }
+  return nt;
+}
+
+// The K2 tasks of a segment, and which kernel runs them (GHOSTM_K2=unit|swar16
+// and GHOSTM_K2_TASKS=paired|consecutive force a choice). With 16-bit integer
+// patterns (swar) the unit-pair kernel is used where its blocks, each ~7 %
+// cheaper (6.5 instead of 7.5 VALU instructions per row pair; same box,
+// cfg 4: 19.00 against 20.30 ms per launch), are at most 1.07x as many as the
+// 16-bit-row kernel's (four queries per block). Its tasks are consecutive runs
+// of two queries unless the pairs make at least 5 % fewer blocks: at equal
+// counts the runs measured faster (cfg 4: 19.0 against 19.5 ms per launch),
+// at 63 candidates per query the pairs (cfg 3: 4.83 against 5.57 ms, 14 %
+// fewer blocks). Only the chosen list is built; the others are counted.
+// `out` has room for ScoreTaskBound(...) tasks.
+inline size_t BuildTasks(bool swar, uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32_t q_end,
+                         const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets,
+                         uint32_t per_block, kern::ScoreTask *out, bool *unit_out) {
+  const char *k2 = getenv("GHOSTM_K2");
+  const char *how = getenv("GHOSTM_K2_TASKS");
+  const bool force_unit = k2 && strcmp(k2, "unit") == 0, force_rows = k2 && strcmp(k2, "swar16") == 0;
+  bool unit = false, paired = false;
+  if (swar && q_end > q_first && !force_rows) {
+    const size_t nc = CountScoreTasks(cand_begin, n, q_first, q_end, counts, offsets, per_block,
+                                      kern::kScoreQmaxUnit);
+    const size_t np = CountPairedTasks(cand_begin, n, q_first, q_end, counts, offsets, per_block);
+    paired = how ? strcmp(how, "paired") == 0 : np * 100 <= nc * 95;
+    const size_t nu = paired ? np : nc;
+    const size_t n4 = CountScoreTasks(cand_begin, n, q_first, q_end, counts, offsets, per_block, kern::kScoreQmax);
+    unit = force_unit || nu * 100 <= n4 * 107;
+    if (getenv("GHOSTM_DEBUG_TASKS"))
+      fprintf(stderr, "k2 tasks: %llu candidates, %u queries: consecutive(2) %zu, paired %zu, consecutive(4) %zu -> %s\n",
+              (unsigned long long)n, q_end - q_first, nc, np, n4, unit ? (paired ? "unit paired" : "unit consecutive") : "rows");
+  }
+  *unit_out = unit;
+  if (unit && paired) return BuildScoreTasksPaired(cand_begin, n, q_first, q_end, counts, offsets, per_block, out);
+  return BuildScoreTasks(cand_begin, n, q_first, q_end, counts, offsets, per_block,
+                         unit ? kern::kScoreQmaxUnit : kern::kScoreQmax, out);
+}
+
+}  // namespace ghostm

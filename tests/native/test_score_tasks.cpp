@@ -1,0 +1,120 @@
+// K2 task lists (ghostm_amd/csrc/score_tasks.h) on random candidate counts:
+// every candidate of the segment is in exactly one task, each task's candidates
+// belong to the queries whose profiles it builds (the unit kernel reads a task
+// as two ranges, the others as one consecutive run over q_first..), and no
+// task exceeds a workgroup.
+#include <cstdio>
+#include <random>
+#include <vector>
+
+#include "../../ghostm_amd/csrc/score_tasks.h"
+
+using ghostm::kern::ScoreTask;
+
+static int Check(const char *what, const std::vector<ScoreTask> &tasks, size_t nt, bool unit, uint32_t qmax,
+                 uint64_t cand_begin, uint64_t n, const std::vector<uint32_t> &qid_of, uint32_t per_block) {
+  std::vector<int> seen(n, 0);
+  for (size_t k = 0; k < nt; ++k) {
+    const ScoreTask &t = tasks[k];
+    if (t.count == 0 || t.count > per_block) { printf("%s: task %zu has %u candidates\n", what, k, t.count); return 1; }
+    for (uint32_t l = 0; l < t.count; ++l) {
+      uint64_t c;
+      uint32_t q;
+      if (unit) {
+        const bool second = l >= t.count1;
+        c = second ? t.begin2 + (l - t.count1) : t.begin + l;
+        q = second ? t.q_second : t.q_first;
+        if (t.q_count != (t.count1 < t.count ? 2u : 1u)) { printf("%s: task %zu q_count\n", what, k); return 1; }
+      } else {
+        c = t.begin + l;
+        q = qid_of[c];
+        if (q < t.q_first || q - t.q_first >= t.q_count || t.q_count > qmax) {
+          printf("%s: task %zu query outside its slots\n", what, k);
+          return 1;
+        }
+      }
+      if (c < cand_begin || c >= cand_begin + n) { printf("%s: task %zu candidate outside\n", what, k); return 1; }
+      if (qid_of[c] != q) { printf("%s: task %zu candidate %llu of query %u read as %u\n", what, k,
+                                   (unsigned long long)c, qid_of[c], q); return 1; }
+      if (seen[c - cand_begin]++) { printf("%s: candidate twice\n", what); return 1; }
+    }
+  }
+  for (uint64_t c = 0; c < n; ++c)
+    if (!seen[c]) { printf("%s: candidate %llu missing\n", what, (unsigned long long)(c + cand_begin)); return 1; }
+  return 0;
+}
+
+int main() {
+  std::mt19937_64 rng(7);
+  const uint32_t per_block = 128, wave_slots = 32;
+  uint64_t trials = 0, paired_waves = 0, consec_waves = 0;
+  for (int trial = 0; trial < 400; ++trial) {
+    const uint32_t nq = 1 + rng() % 400;
+    const double mean = (double)(rng() % 300);
+    std::vector<uint32_t> counts(nq);
+    std::vector<uint64_t> offsets(nq);
+    std::poisson_distribution<uint32_t> pois(mean);
+    uint64_t total = 0;
+    for (uint32_t q = 0; q < nq; ++q) {
+      counts[q] = (rng() % 7 == 0) ? 0 : pois(rng);
+      offsets[q] = total;
+      total += counts[q];
+    }
+    std::vector<uint32_t> qid_of(total);
+    for (uint32_t q = 0; q < nq; ++q)
+      for (uint32_t c = 0; c < counts[q]; ++c) qid_of[offsets[q] + c] = q;
+    if (!total) continue;
+    // a segment: a candidate range that may start and end inside queries
+    const uint64_t b = rng() % total, e = b + 1 + rng() % (total - b);
+    uint32_t q0 = 0, q1 = nq;
+    while (q0 < nq && offsets[q0] + counts[q0] <= b) ++q0;
+    while (q1 > 0 && offsets[q1 - 1] >= e) --q1;
+    const uint64_t n = e - b;
+    for (int mode = 0; mode < 4; ++mode) {
+      const bool unit = true;
+      const uint32_t qmax = 2;
+      std::vector<ScoreTask> tasks(ghostm::ScoreTaskBound(n, q0, q1, per_block, qmax));
+      size_t nt;
+      const char *what;
+      if (mode == 0) {
+        what = "paired";
+        nt = ghostm::BuildScoreTasksPaired(b, n, q0, q1, counts, offsets, per_block, tasks.data());
+        if (nt != ghostm::CountPairedTasks(b, n, q0, q1, counts, offsets, per_block)) {
+          printf("CountPairedTasks %zu disagrees with BuildScoreTasksPaired %zu\n",
+                 ghostm::CountPairedTasks(b, n, q0, q1, counts, offsets, per_block), nt);
+          return 1;
+        }
+      } else if (mode == 1) {
+        what = "consecutive (unit)";
+        nt = ghostm::BuildScoreTasks(b, n, q0, q1, counts, offsets, per_block, qmax, tasks.data());
+      } else if (mode == 2) {
+        what = "consecutive (unit, counted)";
+        nt = ghostm::BuildScoreTasks(b, n, q0, q1, counts, offsets, per_block, qmax, tasks.data());
+        if (nt != ghostm::CountScoreTasks(b, n, q0, q1, counts, offsets, per_block, qmax)) {
+          printf("CountScoreTasks disagrees (two queries)\n");
+          return 1;
+        }
+      } else {
+        what = "chosen kernel";
+        bool unit_k = false;
+        nt = ghostm::BuildTasks(true, b, n, q0, q1, counts, offsets, per_block, tasks.data(), &unit_k);
+        if (Check(what, tasks, nt, unit_k, unit_k ? 2u : 4u, b, n, qid_of, per_block)) return 1;
+        if (!unit_k && nt != ghostm::CountScoreTasks(b, n, q0, q1, counts, offsets, per_block, 4)) {
+          printf("CountScoreTasks disagrees with BuildScoreTasks\n");
+          return 1;
+        }
+        ++trials;
+        continue;
+      }
+      if (nt > tasks.size()) { printf("%s: %zu tasks over the bound %zu\n", what, nt, tasks.size()); return 1; }
+      if (Check(what, tasks, nt, unit, qmax, b, n, qid_of, per_block)) return 1;
+      uint64_t w = 0;
+      for (size_t k = 0; k < nt; ++k) w += (tasks[k].count + wave_slots - 1) / wave_slots;
+      if (mode == 0) paired_waves += w;
+      if (mode == 1) consec_waves += w;
+    }
+  }
+  printf("%llu trials ok; waves: paired %llu, consecutive %llu\n", (unsigned long long)trials,
+         (unsigned long long)paired_waves, (unsigned long long)consec_waves);
+  return 0;
+}

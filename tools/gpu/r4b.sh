@@ -19,3 +19,6 @@ for p in cfg3 cfg4; do
     python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], round(d['ms_per_step'],2), round(d['roofline']['avg_launch_ms'],3), round(d['roofline']['frac'],4), d['full_output_matches_reference'])" gpurun_out/r4b/ab_${p}_$1_$2.json
   done
 done
+# K3a scan: unpacked row offsets (this build) against the previous build
+AB_ROUNDS=2 timeout -k 10 400 bash tools/ab.sh prev > gpurun_out/r4b/ab_scan.txt 2>&1 || exit $?
+cat gpurun_out/r4b/ab_scan.txt
