@@ -450,6 +450,11 @@ def main() -> None:
             # would free its page-cache pages inside the timed region)
             if rank == 0 and os.path.exists(out_path):
                 os.remove(out_path)
+            # every run starts from a clean page cache, as the first one does: the
+            # previous run's dirty output pages are written back here, untimed
+            # (left dirty, their writeback throttled the next run's writes and
+            # reads: cfg3 runs took 37, 44 and 53 ms in a row, profiles/r4l_e2e_*)
+            os.sync()
             if dist is not None:
                 dist.barrier()
             te = time.perf_counter()

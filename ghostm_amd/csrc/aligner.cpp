@@ -1107,69 +1107,39 @@ inline char *PutStr(char *p, const std::string &s) {
   std::memcpy(p, s.data(), s.size());
   return p + s.size();
 }
-inline std::string FloatText(float f) {
-  char buf[48];
-  return std::string(buf, PutFloat(buf, f));
+// %g text of at most 15 bytes (every float's fits: "-1.17549e-38" is 12)
+inline char *PutFloat15(char *p, float f) {
+  return std::to_chars(p, p + 15, f, std::chars_format::general, 6).ptr;
 }
 constexpr uint32_t kIdLen = 512, kIdMatch = 128;
 }  // namespace
 
-// One output line, WriteOutput / V1 / V2 (aligner.cpp:951-1012). Everything that
-// depends only on the score (bits, exp(-lambda*s)) or only on (len, matches)
-// (the identity) is formatted once per session; per hit only the E-value is
-// computed and formatted, with the reference's float/double steps.
-struct LineFormat {
-  int style = 0;
-  EvalueCalculator ev;
-  std::vector<std::string> bits_txt;  // per score
-  std::vector<double> expd;           // per score: exp(-1.0 * s * lambda)
-  std::vector<std::string> id_txt;    // per (len, match): 100*id (style 0) or id (style 2)
-  // E-value text per (query length, score): the E-value depends on nothing
-  // else (search space = qlen x the DB's residue sum), so each one is formatted
-  // once per session, by whichever formatter thread needs it first. Entry:
-  // byte 0 = text length (0: not yet), bytes 1..15 = the text; racing writers
-  // store the same bytes.
-  struct EvText {
-    std::atomic<uint64_t> a{0}, b{0};
+// A table of short texts (at most 15 bytes) filled on first use: entry = byte 0
+// the length (0: not yet), bytes 1..15 the text, in two 64-bit atomics; racing
+// writers store the same bytes. The storage comes zeroed from calloc (the OS's
+// zero pages), so a table costs nothing until entries are used: the session's
+// create → run path no longer formats 60 K identity strings up front.
+struct TextCache {
+  struct Entry {
+    std::atomic<uint64_t> a, b;
   };
-  static constexpr uint32_t kEvScores = 4096;
-  mutable std::unique_ptr<EvText[]> ev_txt;
-
-  LineFormat(int st, const KarlinParams &k, uint32_t max_score) : style(st), ev(k) {
-    if (style == 0) {
-      bits_txt.resize(max_score + 1);
-      expd.resize(max_score + 1);
-      for (uint32_t sc = 0; sc <= max_score; ++sc) {
-        bits_txt[sc] = FloatText(ev.Bits((int)sc));
-        expd[sc] = exp(static_cast<double>(-1.0 * (int)sc * ev.p.lambda));
-      }
-      ev_txt.reset(new EvText[(size_t)(kMaxQueryLength + 1) * kEvScores]);
-    }
-    if (style != 1) {
-      id_txt.resize(kIdLen * kIdMatch);
-      for (uint32_t len = 1; len < kIdLen; ++len)
-        for (uint32_t m = 0; m < kIdMatch && m <= len; ++m) id_txt[len * kIdMatch + m] = FloatText(Id(len, m));
-    }
+  Entry *e = nullptr;
+  size_t n = 0;
+  explicit TextCache(size_t entries) : e(static_cast<Entry *>(std::calloc(entries, sizeof(Entry)))), n(entries) {
+    if (!e) throw std::bad_alloc();
   }
-  float Id(uint32_t len, uint32_t m) const {
-    const float id = (float)m / (float)len;  // aligner.cpp:945
-    return style == 0 ? id * 100 : id;
-  }
-  char *PutId(char *p, uint32_t len, uint32_t m) const {
-    if (len < kIdLen && m < kIdMatch && m <= len && len > 0) return PutStr(p, id_txt[len * kIdMatch + m]);
-    return PutFloat(p, Id(len, m));
-  }
-  // the E-value (float)((double)scaled * exp(-lambda * score)), as %g text
-  char *PutEvalue(char *p, uint32_t qlen, uint32_t score, float scaled) const {
-    const double e = score < expd.size() ? expd[score] : exp(static_cast<double>(-1.0 * (int)score * ev.p.lambda));
-    if (qlen > kMaxQueryLength || score >= kEvScores || !ev_txt) return PutFloat(p, (float)((double)scaled * e));
-    EvText &c = ev_txt[(size_t)qlen * kEvScores + score];
+  ~TextCache() { std::free(e); }
+  TextCache(const TextCache &) = delete;
+  TextCache &operator=(const TextCache &) = delete;
+  // the text of entry k, made by make(buf) (writes at most 15 bytes, returns its end) on first use
+  template <class F>
+  char *Put(char *p, size_t k, F make) const {
+    Entry &c = e[k];
     uint64_t w[2];
     w[0] = c.a.load(std::memory_order_acquire);
     if (w[0] == 0) {
       char buf[16] = {0};
-      char *end = std::to_chars(buf + 1, buf + 16, (float)((double)scaled * e), std::chars_format::general, 6).ptr;
-      buf[0] = (char)(end - buf - 1);
+      buf[0] = (char)(make(buf + 1) - (buf + 1));
       std::memcpy(w, buf, 16);
       c.b.store(w[1], std::memory_order_relaxed);
       c.a.store(w[0], std::memory_order_release);
@@ -1180,6 +1150,52 @@ struct LineFormat {
     std::memcpy(buf, w, 16);
     std::memcpy(p, buf + 1, 15);  // the line buffer has kFixed bytes of room
     return p + (unsigned char)buf[0];
+  }
+};
+
+// One output line, WriteOutput / V1 / V2 (aligner.cpp:951-1012). Everything that
+// depends only on the score (bits, exp(-lambda*s)), only on (len, matches) (the
+// identity) or only on (query length, score) (the E-value: search space = qlen x
+// the DB's residue sum) is formatted once per session, by whichever formatter
+// thread needs it first (TextCache); the arithmetic is the reference's float /
+// double steps.
+struct LineFormat {
+  int style = 0;
+  EvalueCalculator ev;
+  std::vector<double> expd;           // per score: exp(-1.0 * s * lambda)
+  static constexpr uint32_t kEvScores = 4096;
+  std::unique_ptr<TextCache> bits_txt;  // per score
+  std::unique_ptr<TextCache> id_txt;    // per (len, match): 100*id (style 0) or id (style 2)
+  std::unique_ptr<TextCache> ev_txt;    // per (query length, score)
+
+  LineFormat(int st, const KarlinParams &k, uint32_t max_score) : style(st), ev(k) {
+    if (style == 0) {
+      expd.resize(max_score + 1);
+      for (uint32_t sc = 0; sc <= max_score; ++sc) expd[sc] = exp(static_cast<double>(-1.0 * (int)sc * ev.p.lambda));
+      bits_txt.reset(new TextCache(max_score + 1));
+      ev_txt.reset(new TextCache((size_t)(kMaxQueryLength + 1) * kEvScores));
+    }
+    if (style != 1) id_txt.reset(new TextCache((size_t)kIdLen * kIdMatch));
+  }
+  float Id(uint32_t len, uint32_t m) const {
+    const float id = (float)m / (float)len;  // aligner.cpp:945
+    return style == 0 ? id * 100 : id;
+  }
+  char *PutId(char *p, uint32_t len, uint32_t m) const {
+    if (len < kIdLen && m < kIdMatch && m <= len && len > 0)
+      return id_txt->Put(p, (size_t)len * kIdMatch + m, [&](char *b) { return PutFloat15(b, Id(len, m)); });
+    return PutFloat(p, Id(len, m));
+  }
+  // the E-value (float)((double)scaled * exp(-lambda * score)), as %g text
+  char *PutEvalue(char *p, uint32_t qlen, uint32_t score, float scaled) const {
+    const double e = score < expd.size() ? expd[score] : exp(static_cast<double>(-1.0 * (int)score * ev.p.lambda));
+    if (qlen > kMaxQueryLength || score >= kEvScores || !ev_txt) return PutFloat(p, (float)((double)scaled * e));
+    return ev_txt->Put(p, (size_t)qlen * kEvScores + score, [&](char *b) { return PutFloat15(b, (float)((double)scaled * e)); });
+  }
+  char *PutBits(char *p, uint32_t score) const {
+    if (bits_txt && score < bits_txt->n)
+      return bits_txt->Put(p, score, [&](char *b) { return PutFloat15(b, ev.Bits((int)score)); });
+    return PutFloat(p, ev.Bits((int)score));
   }
   // bytes a line can take beyond the two names
   static constexpr size_t kFixed = 160;
@@ -1208,9 +1224,7 @@ struct LineFormat {
       p = PutU32(p, start + 1); *p++ = '\t';
       p = PutU32(p, end + 1); *p++ = '\t';
       p = PutEvalue(p, qlen, score, scaled); *p++ = '\t';
-      if (score < bits_txt.size()) p = PutStr(p, bits_txt[score]);
-      else p = PutFloat(p, ev.Bits((int)score));
-      *p++ = '\t';
+      p = PutBits(p, score); *p++ = '\t';
     }
     *p++ = '\n';
     return p;
