@@ -277,8 +277,8 @@ uint64_t CountsHash(const uint32_t *c, size_t n) {
 }  // namespace
 
 // Name groups (consecutive equal names, merged into one result list:
-// aligner.cpp:697-700) and WriteOutput's query lengths of one query chunk.
-void Session::PrepareQueryChunk(QueryData *qd) {
+// aligner.cpp:697-700) and (qlen) WriteOutput's query lengths of one query chunk.
+void Session::PrepareQueryChunk(QueryData *qd, bool qlen) {
   QueryData &q = *qd;
   const uint32_t n = q.chunk.nseq, L = q.chunk.L;
   q.group_end.assign(n, 0);
@@ -291,8 +291,28 @@ void Session::PrepareQueryChunk(QueryData *qd) {
     q.group_first.push_back(i);
     q.group_last.push_back(q.group_end[i] - 1);
   }
+  if (!qlen) return;
   q.qlen.assign(n, 1);
   for (uint32_t i = 0; i < n; ++i) q.qlen[i] = QueryResidues(&q.chunk.seq[(size_t)i * L], L);
+}
+
+// WriteOutput's query lengths of every loaded chunk on the worker pool, in
+// blocks of rows (a row's last byte per 127: ~9 ms per 500 K-query chunk on one
+// thread, the largest part of reading a chunk once its names are a NameTable).
+void Session::QueryLengths(std::vector<QueryData *> chunks) {
+  constexpr uint32_t kRows = 1u << 15;
+  std::vector<std::pair<QueryData *, uint32_t>> blocks;
+  for (QueryData *q : chunks) {
+    q->qlen.assign(q->chunk.nseq, 1);
+    for (uint32_t r = 0; r < q->chunk.nseq; r += kRows) blocks.emplace_back(q, r);
+  }
+  ParallelFor(blocks.size(), std::max(1u, threads_), [&](size_t b, size_t e, unsigned) {
+    for (size_t k = b; k < e; ++k) {
+      QueryData &q = *blocks[k].first;
+      const uint32_t L = q.chunk.L, r1 = std::min(q.chunk.nseq, blocks[k].second + kRows);
+      for (uint32_t i = blocks[k].second; i < r1; ++i) q.qlen[i] = QueryResidues(&q.chunk.seq[(size_t)i * L], L);
+    }
+  });
 }
 
 // The batch plan of a slice against DB chunk di, from the counts of its WHOLE
@@ -361,7 +381,7 @@ void Session::ApplyShard(uint32_t rank, uint32_t world) {
         }
       }
       c.seq.Own(std::vector<uint8_t>(c.seq.begin() + (size_t)i0 * c.L, c.seq.begin() + (size_t)(i0 + n) * c.L));
-      c.names = std::vector<std::string>(c.names.begin() + i0, c.names.begin() + i0 + n);
+      c.names = c.names.Slice(i0, n);
       c.nseq = n;
       q.global_base += i0;
       PrepareQueryChunk(&q);
@@ -573,6 +593,15 @@ void Session::Load(uint32_t shard_rank, uint32_t shard_world, bool local, std::v
   TraceMark("create");
   dev.Bind(opt_.device);
   TraceMark("bound");
+  // the staged uploads' host copies on the worker pool, 1 MB per piece
+  const unsigned copiers = std::max(1u, std::min(threads_, 8u));
+  dev.SetHostCopy([copiers](void *dst, const void *src, size_t n) {
+    const size_t piece = 1u << 20, pieces = (n + piece - 1) / piece;
+    ParallelFor(pieces, copiers, [&](size_t b, size_t e, unsigned) {
+      const size_t lo = b * piece, hi = std::min(n, e * piece);
+      std::memcpy(static_cast<char *>(dst) + lo, static_cast<const char *>(src) + lo, hi - lo);
+    });
+  });
   dev.SetMatrix(opt_.matrix.m.data());
 
   // query chunks: -S start (or 0) .. -L end, as Execute walks them
@@ -608,7 +637,7 @@ void Session::Load(uint32_t shard_rank, uint32_t shard_world, bool local, std::v
                     qok[k] = qf.IndexChunk(id + (uint32_t)k, &qidx[k]);
                   } else if (k < nq_chunks) {
                     qok[k] = qf.ReadChunk(id + (uint32_t)k, &qread[k].chunk);
-                    if (qok[k]) PrepareQueryChunk(&qread[k]);
+                    if (qok[k]) PrepareQueryChunk(&qread[k], false);
                   } else {
                     dok[k - nq_chunks] = df.ReadChunk((uint32_t)(k - nq_chunks), &dread[k - nq_chunks].chunk);
                   }
@@ -617,6 +646,11 @@ void Session::Load(uint32_t shard_rank, uint32_t shard_world, bool local, std::v
   uint32_t nchunks = 0;
   while (nchunks < nq_chunks && qok[nchunks]) ++nchunks;
   if (nchunks == 0) throw std::runtime_error("[Aligner] error: don't find query file.");
+  if (!local) {
+    std::vector<QueryData *> chunks;
+    for (uint32_t k = 0; k < nchunks; ++k) chunks.push_back(&qread[k]);
+    QueryLengths(chunks);
+  }
   TraceMark("queries_read", nchunks);
 
   db_sum_u32_ = (uint32_t)df.sum_length;
@@ -683,9 +717,14 @@ void Session::Load(uint32_t shard_rank, uint32_t shard_world, bool local, std::v
         const uint32_t k = read[j];
         qidx[k].ReadSlice(qread[k].slice_lo, (uint32_t)(rank_lo[k][shard_rank + 1] - qread[k].slice_lo),
                           &qread[k].chunk);
-        PrepareQueryChunk(&qread[k]);
+        PrepareQueryChunk(&qread[k], false);
       }
     });
+    {
+      std::vector<QueryData *> chunks;
+      for (uint32_t k : read) chunks.push_back(&qread[k]);
+      QueryLengths(chunks);
+    }
     for (uint32_t k : read) queries_.push_back(std::move(qread[k]));
     TraceMark("slices_read", queries_.size());
   } else {
@@ -1103,7 +1142,7 @@ inline char *PutU32(char *p, uint32_t v) {
 inline char *PutFloat(char *p, float f) {
   return std::to_chars(p, p + 48, f, std::chars_format::general, 6).ptr;
 }
-inline char *PutStr(char *p, const std::string &s) {
+inline char *PutStr(char *p, std::string_view s) {
   std::memcpy(p, s.data(), s.size());
   return p + s.size();
 }
@@ -1200,7 +1239,7 @@ struct LineFormat {
   // bytes a line can take beyond the two names
   static constexpr size_t kFixed = 160;
   // scaled = (float)search_space * K, per query of non-X length qlen
-  char *Write(char *p, const std::string &qname, const std::string &sname, uint32_t score, uint32_t start,
+  char *Write(char *p, std::string_view qname, std::string_view sname, uint32_t score, uint32_t start,
               uint32_t end, uint32_t len, uint32_t match, float scaled, uint32_t qlen) const {
     p = PutStr(p, qname);
     *p++ = '\t';
@@ -1273,10 +1312,10 @@ void Session::FormatResults(const QueryData &q, const Results &results, Part *ou
     for (size_t i = b; i < e; ++i) {
       const uint64_t space = (uint64_t)q.qlen[i] * (uint64_t)db_sum_u32_;
       const float scaled = (float)space * w.ev.p.K;
-      const std::string &qname = q.chunk.names[i];
+      const std::string_view qname = q.chunk.names[i];
       for (const HitRecord &h : results[i]) {
         const DbData &d = dbs_[h.db_chunk];
-        const std::string &sname = d.chunk.names[h.subject];
+        const std::string_view sname = d.chunk.names[h.subject];
         char *p = text.Reserve(qname.size() + sname.size() + LineFormat::kFixed);
         text.Commit(w.Write(p, qname, sname, h.score, h.start, h.end, h.aln_len, h.aln_match, scaled, q.qlen[i]));
         hits.push_back(GhostmHit{q.global_base + (uint32_t)i, d.global_base + h.subject, h.score, h.start,
@@ -1303,7 +1342,7 @@ void Session::FormatSelected(const QueryData &q, uint32_t g0, const std::vector<
     TextCursor text(out->text[t]);
     for (size_t g = b; g < e; ++g) {
       const uint32_t i = q.group_last[g0 + g];
-      const std::string &name = q.chunk.names[i];
+      const std::string_view name = q.chunk.names[i];
       const uint64_t space = (uint64_t)q.qlen[i] * (uint64_t)db_sum_u32_;
       const float scaled = (float)space * w.ev.p.K;
       for (uint32_t k = 0; k < counts[g]; ++k) {
@@ -1311,7 +1350,7 @@ void Session::FormatSelected(const QueryData &q, uint32_t g0, const std::vector<
         const DbData &d = dbs_[h.chunk];
         const uint32_t len = h.ml >> 8, match = h.ml & 0xFFu;
         const float seq_id = (float)match / (float)len;  // aligner.cpp:945
-        const std::string &sname = d.chunk.names[h.sid];
+        const std::string_view sname = d.chunk.names[h.sid];
         char *p = text.Reserve(name.size() + sname.size() + LineFormat::kFixed);
         text.Commit(w.Write(p, name, sname, h.score, h.start, h.end, len, match, scaled, q.qlen[i]));
         ph.push_back(GhostmHit{q.global_base + i, d.global_base + h.sid, h.score, h.start, h.end, len, match,

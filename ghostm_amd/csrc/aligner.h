@@ -174,7 +174,8 @@ class Session {
   };
   using Results = std::vector<std::vector<HitRecord>>;
 
-  static void PrepareQueryChunk(QueryData *q);
+  static void PrepareQueryChunk(QueryData *q, bool qlen = true);
+  void QueryLengths(std::vector<QueryData *> chunks);
   void ApplyShard(uint32_t rank, uint32_t world);
   // shard sessions: the batch plan of every (query chunk, DB chunk)
   void PlanFromCounts(QueryData &q, size_t di, const std::vector<uint32_t> &chunk_counts, uint32_t n);

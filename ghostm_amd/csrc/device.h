@@ -11,6 +11,7 @@
 #pragma once
 #include <cstddef>
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <string>
 #include <vector>
@@ -98,6 +99,11 @@ class DeviceModule {
   std::string DeviceName() const;
   size_t TotalMemory() const;
 
+  // Copies n bytes host to host (the session sets a parallel one; default memcpy).
+  using HostCopyFn = std::function<void(void *dst, const void *src, size_t n)>;
+  void SetHostCopy(HostCopyFn fn);
+  // Host to device through page-locked staging on the main stream (see device.hip).
+  void StagedUpload(void *dst, const void *src, size_t bytes);
   DevQuery *UploadQuery(const uint8_t *seq, uint32_t nseq, uint32_t L);
   DevDb *UploadDb(const uint8_t *seq, uint32_t len, const uint32_t *keys_count, uint32_t kcl,
                   const uint32_t *positions, uint32_t npos);
@@ -196,6 +202,7 @@ class DeviceModule {
   void LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, const DevDb *d, uint32_t span);
   int device_ = -1;
   void *stream_ = nullptr;
+  HostCopyFn host_copy_;
   void *copy_stream_ = nullptr;  // D2H of selections and K2 task uploads, beside the kernels
   DeviceTimes times_;
   uint64_t records_ = 0;

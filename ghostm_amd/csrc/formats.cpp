@@ -5,6 +5,7 @@
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
+#include <emmintrin.h>
 
 #include <algorithm>
 #include <climits>
@@ -110,48 +111,97 @@ static void ReadRaw(std::ifstream &f, T *p, size_t count) {
   f.read(reinterpret_cast<char *>(p), sizeof(T) * count);
 }
 
-std::vector<std::string> ReadNameLines(const std::string &path, uint32_t n, bool *complete) {
-  std::vector<std::string> names(n);
+void NameTable::push_back(std::string_view s) {
+  if (!own_) {
+    auto o = std::make_shared<std::string>();
+    if (!end_.empty()) o->assign(Base(), end_.back() + 1);
+    own_ = o;
+    hold_.reset();
+    data_ = nullptr;
+  }
+  own_->append(s.data(), s.size());
+  if (own_->size() > UINT32_MAX) throw std::length_error("sequence names over 4 GB");
+  end_.push_back((uint32_t)own_->size());
+  own_->push_back('\n');
+}
+
+void NameTable::AdoptLines(std::shared_ptr<const void> hold, const char *data, std::vector<uint32_t> ends) {
+  *this = NameTable();
+  hold_ = std::move(hold);
+  data_ = data;
+  end_ = std::move(ends);
+}
+
+NameTable NameTable::Slice(size_t i0, size_t n) const {
+  NameTable t;
+  if (n == 0) return t;
+  const uint32_t b = i0 ? end_[i0 - 1] + 1 : 0;
+  std::vector<uint32_t> ends(n);
+  for (size_t k = 0; k < n; ++k) ends[k] = end_[i0 + k] - b;
+  auto own = std::make_shared<std::string>(Base() + b, (size_t)(end_[i0 + n - 1] + 1 - b));
+  t.AdoptLines(own, own->data(), std::move(ends));
+  return t;
+}
+
+// Offsets of the first `want` newlines of buf (16 bytes per compare: names are
+// ~8 bytes, so a memchr per line spent most of its time on call overhead).
+static void FindNewlines(const char *buf, size_t size, uint32_t want, std::vector<uint32_t> *out) {
+  out->reserve(want);
+  size_t i = 0;
+  const __m128i nl = _mm_set1_epi8('\n');
+  for (; i + 16 <= size && out->size() < want; i += 16) {
+    uint32_t m = (uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_loadu_si128(reinterpret_cast<const __m128i *>(buf + i)), nl));
+    while (m && out->size() < want) {
+      out->push_back((uint32_t)(i + (uint32_t)__builtin_ctz(m)));
+      m &= m - 1;
+    }
+  }
+  for (; i < size && out->size() < want; ++i)
+    if (buf[i] == '\n') out->push_back((uint32_t)i);
+}
+
+NameTable ReadNameLines(const std::string &path, uint32_t n, bool *complete) {
+  NameTable names;
   if (complete) *complete = true;
   {
-    // the whole file in one read, split at the first n newlines: the same
-    // strings as the getline loop below whenever the file holds n terminated
-    // lines (the usual case); anything shorter takes that loop
-    std::ifstream b(path.c_str(), std::ios::binary);
-    if (!b) return names;
-    b.seekg(0, std::ios::end);
-    const std::streamoff size = b.tellg();
-    if (size > 0) {
-      std::string all((size_t)size, '\0');
-      b.seekg(0);
-      b.read(&all[0], size);
-      if (b.gcount() == size) {
-        std::vector<size_t> ends;
-        ends.reserve(n);
-        for (size_t at = all.find('\n'); at != std::string::npos && ends.size() < n; at = all.find('\n', at + 1))
-          ends.push_back(at);
+    // the file mapped, split at its first n newlines: the same names as the
+    // getline loop below whenever the file holds n terminated lines (the usual
+    // case); anything shorter takes that loop
+    const int fd = open(path.c_str(), O_RDONLY);
+    if (fd < 0) {
+      for (uint32_t i = 0; i < n; ++i) names.push_back(std::string_view());
+      return names;
+    }
+    struct stat st {};
+    if (n && fstat(fd, &st) == 0 && st.st_size > 0 && (uint64_t)st.st_size <= UINT32_MAX) {
+      const size_t len = (size_t)st.st_size;
+      void *m = mmap(nullptr, len, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+      if (m != MAP_FAILED) {
+        std::shared_ptr<const void> hold(m, [len](const void *q) { munmap(const_cast<void *>(q), len); });
+        std::vector<uint32_t> ends;
+        FindNewlines(static_cast<const char *>(m), len, n, &ends);
         if (ends.size() == n) {
-          size_t from = 0;
-          for (uint32_t i = 0; i < n; ++i) {
-            names[i].assign(all, from, ends[i] - from);
-            from = ends[i] + 1;
-          }
+          close(fd);
+          names.AdoptLines(std::move(hold), static_cast<const char *>(m), std::move(ends));
           return names;
         }
       }
     }
+    close(fd);
   }
   std::ifstream f(path.c_str());
-  if (!f) return names;
   uint32_t i = 0;
   std::string line;
-  for (; i < n && !f.eof(); ++i) {
-    std::getline(f, line);
-    names[i].swap(line);
+  if (f) {
+    for (; i < n && !f.eof(); ++i) {
+      std::getline(f, line);
+      names.push_back(line);
+    }
   }
   if (i < n) {
-    std::cerr << "warning : couldn't read all sequence names" << std::endl;
+    if (f) std::cerr << "warning : couldn't read all sequence names" << std::endl;
     if (complete) *complete = false;
+    for (; i < n; ++i) names.push_back(std::string_view());  // the missing names read as empty
   }
   return names;
 }
@@ -271,11 +321,15 @@ void QueryChunkIndex::ReadSlice(uint32_t i0, uint32_t n, QueryChunk *q) const {
   q->id = id;
   q->nseq = n;
   q->L = L;
-  q->names.resize(n);
-  for (uint32_t k = 0; k < n; ++k) {
-    const uint32_t i = i0 + k;
-    if (!names.empty()) q->names[k] = names[i];
-    else q->names[k].assign(nam, line[i], line[i + 1] - 1 - line[i]);
+  if (!names.empty()) {
+    q->names = names.Slice(i0, n);
+  } else {
+    // the slice's lines of the .nam bytes
+    const uint64_t b = line[i0], e = line[i0 + n];
+    std::vector<uint32_t> ends(n);
+    for (uint32_t k = 0; k < n; ++k) ends[k] = (uint32_t)(line[i0 + k + 1] - 1 - b);
+    auto own = std::make_shared<std::string>(nam, b, e - b);
+    q->names.AdoptLines(own, own->data(), std::move(ends));
   }
   // (a short file leaves zeros, as ReadChunk)
   q->seq.Map(base + ".seq", (uint64_t)i0 * L, (size_t)n * L);

@@ -12,9 +12,40 @@
 #include <cstdint>
 #include <memory>
 #include <string>
+#include <string_view>
 #include <vector>
 
 namespace ghostm {
+
+// Sequence names of a chunk: the .nam file's own bytes (a read-only mapping of
+// its page-cache pages: no copy, no zero-filled buffer) and the offset of each
+// name's newline, instead of one std::string per name (cfg 4's 1 M query names
+// took ~10 ms per query chunk to build as strings, most of the session's file
+// loading). Names added one by one (the getline path, slices) are kept in an
+// owned buffer in the same layout: each name followed by one separator byte.
+class NameTable {
+ public:
+  size_t size() const { return end_.size(); }
+  bool empty() const { return end_.empty(); }
+  std::string_view operator[](size_t i) const {
+    const uint32_t b = i ? end_[i - 1] + 1 : 0;
+    return std::string_view(Base() + b, (size_t)(end_[i] - b));
+  }
+  void clear() { *this = NameTable(); }
+  void push_back(std::string_view s);
+  // the lines of a mapped or owned buffer: name i ends at ends[i] (excluded),
+  // the next one starts at ends[i] + 1
+  void AdoptLines(std::shared_ptr<const void> hold, const char *data, std::vector<uint32_t> ends);
+  // names [i0, i0 + n) as a table of their own
+  NameTable Slice(size_t i0, size_t n) const;
+
+ private:
+  const char *Base() const { return own_ ? own_->data() : data_; }
+  std::shared_ptr<const void> hold_;    // the mapping (or an owned buffer) data_ points into
+  const char *data_ = nullptr;
+  std::shared_ptr<std::string> own_;    // names added one by one
+  std::vector<uint32_t> end_;           // name i = [end_[i - 1] + 1, end_[i])
+};
 
 // A read-only array of a chunk file's contents: a private, pre-faulted mapping
 // of the file (its page-cache pages: no copy, no zero-fill page faults), or
@@ -45,7 +76,7 @@ struct QueryChunk {
   uint32_t id = 0;
   uint32_t nseq = 0;
   uint32_t L = 0;                  // fixed record width (X padded)
-  std::vector<std::string> names;  // one per record
+  NameTable names;                 // one per record
   FileArray<uint8_t> seq;          // nseq * L codes
 };
 
@@ -67,7 +98,7 @@ struct QueryChunkIndex {
   std::string base;                    // <prefix>_<id>
   std::string nam;                     // the .nam file, when it holds nseq terminated lines
   std::vector<uint64_t> line;          // line k = nam[line[k], line[k + 1] - 1)
-  std::vector<std::string> names;      // otherwise every name, read the reference's way
+  NameTable names;                     // otherwise every name, read the reference's way
 };
 
 struct QueryFile {
@@ -84,7 +115,7 @@ struct DbChunk {
   uint32_t id = 0;
   uint32_t nseq = 0;
   uint32_t len = 0;                // concatenated length incl. END separators
-  std::vector<std::string> names;
+  NameTable names;
   std::vector<uint32_t> starts;    // subject start offsets (.pos)
   FileArray<uint8_t> seq;
   uint32_t seed = 0, kcl = 0, npos = 0;
@@ -107,6 +138,6 @@ struct DbFile {
 uint32_t SeedLength(uint32_t seed);
 uint32_t SeedWeight(uint32_t seed);
 
-std::vector<std::string> ReadNameLines(const std::string &path, uint32_t n, bool *complete);
+NameTable ReadNameLines(const std::string &path, uint32_t n, bool *complete);
 
 }  // namespace ghostm
