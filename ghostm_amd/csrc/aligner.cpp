@@ -1153,11 +1153,15 @@ inline char *PutFloat15(char *p, float f) {
 constexpr uint32_t kIdLen = 512, kIdMatch = 128;
 }  // namespace
 
-// A table of short texts (at most 15 bytes) filled on first use: entry = byte 0
-// the length (0: not yet), bytes 1..15 the text, in two 64-bit atomics; racing
-// writers store the same bytes. The storage comes zeroed from calloc (the OS's
-// zero pages), so a table costs nothing until entries are used: the session's
-// create → run path no longer formats 60 K identity strings up front.
+// A table of short texts (at most 15 bytes) filled on first use: entry = bytes
+// 0..14 the text, byte 15 its length (0: not yet), in two 64-bit atomics (the
+// second, holding the length, published last); racing writers store the same
+// bytes. A hit copies the 16 bytes straight from the two loaded words into the
+// line (which has kFixed bytes of room) and steps on by the length: no reload
+// from a stack buffer at an odd offset, which stalled on store forwarding. The
+// storage comes zeroed from calloc (the OS's zero pages), so a table costs
+// nothing until entries are used: the session's create -> run path no longer
+// formats 60 K identity strings up front.
 struct TextCache {
   struct Entry {
     std::atomic<uint64_t> a, b;
@@ -1175,20 +1179,18 @@ struct TextCache {
   char *Put(char *p, size_t k, F make) const {
     Entry &c = e[k];
     uint64_t w[2];
-    w[0] = c.a.load(std::memory_order_acquire);
-    if (w[0] == 0) {
+    w[1] = c.b.load(std::memory_order_acquire);
+    if ((w[1] >> 56) == 0) {
       char buf[16] = {0};
-      buf[0] = (char)(make(buf + 1) - (buf + 1));
+      buf[15] = (char)(make(buf) - buf);
       std::memcpy(w, buf, 16);
-      c.b.store(w[1], std::memory_order_relaxed);
-      c.a.store(w[0], std::memory_order_release);
+      c.a.store(w[0], std::memory_order_relaxed);
+      c.b.store(w[1], std::memory_order_release);
     } else {
-      w[1] = c.b.load(std::memory_order_relaxed);
+      w[0] = c.a.load(std::memory_order_relaxed);
     }
-    char buf[16];
-    std::memcpy(buf, w, 16);
-    std::memcpy(p, buf + 1, 15);  // the line buffer has kFixed bytes of room
-    return p + (unsigned char)buf[0];
+    std::memcpy(p, w, 16);
+    return p + (w[1] >> 56);
   }
 };
 

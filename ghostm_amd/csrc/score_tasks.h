@@ -86,32 +86,46 @@ inline size_t BuildScoreTasksPaired(uint64_t cand_begin, uint64_t n, uint32_t q_
     t.q_second = q;
     out[nt++] = t;
   };
-  // remainders by size (1 .. per_block - 1): stacks of (query, first candidate)
-  std::vector<std::vector<std::pair<uint32_t, uint64_t>>> rem(per_block);
+  // the remainders (query, first candidate) grouped by size with a counting
+  // sort (flat arrays; a per-size stack of vectors cost ~1 ms per segment on
+  // the critical path of a chunk's first segment)
   const uint64_t cand_end = cand_begin + n;
+  std::vector<uint32_t> start(per_block + 1, 0);
+  auto range = [&](uint32_t qi, uint64_t *lo, uint64_t *hi) {
+    *lo = std::max<uint64_t>(offsets[qi], cand_begin);
+    *hi = std::min<uint64_t>(offsets[qi] + counts[qi], cand_end);
+  };
   for (uint32_t qi = q_first; qi < q_end; ++qi) {
-    uint64_t lo = std::max<uint64_t>(offsets[qi], cand_begin);
-    const uint64_t hi = std::min<uint64_t>(offsets[qi] + counts[qi], cand_end);
+    uint64_t lo, hi;
+    range(qi, &lo, &hi);
+    if (lo < hi && (hi - lo) % per_block) ++start[(hi - lo) % per_block + 1];
+  }
+  for (uint32_t r = 1; r <= per_block; ++r) start[r] += start[r - 1];
+  std::vector<uint32_t> top(start.begin(), start.end() - 1);  // fill cursor per size
+  std::vector<std::pair<uint32_t, uint64_t>> rem(start[per_block]);
+  for (uint32_t qi = q_first; qi < q_end; ++qi) {
+    uint64_t lo, hi;
+    range(qi, &lo, &hi);
     if (lo >= hi) continue;
     while (hi - lo >= per_block) {
       single(qi, lo, per_block);
       lo += per_block;
     }
-    if (hi > lo) rem[hi - lo].emplace_back(qi, lo);
+    if (hi > lo) rem[top[hi - lo]++] = {qi, lo};
   }
+  // greedy best fit, largest first; a size's entries are taken from the end
+  // of its range (top[r] = one past the last unused entry of size r)
   for (uint32_t r1 = per_block - 1; r1 >= 1; --r1) {
-    while (!rem[r1].empty()) {
-      const std::pair<uint32_t, uint64_t> a = rem[r1].back();
-      rem[r1].pop_back();
+    while (top[r1] > start[r1]) {
+      const std::pair<uint32_t, uint64_t> a = rem[--top[r1]];
       uint32_t pick = 0;
       for (uint32_t r2 = std::min(r1, per_block - r1); r2 >= 1 && !pick; --r2)
-        if (!rem[r2].empty()) pick = r2;
+        if (top[r2] > start[r2]) pick = r2;
       if (!pick) {
         single(a.first, a.second, r1);
         continue;
       }
-      const std::pair<uint32_t, uint64_t> b = rem[pick].back();
-      rem[pick].pop_back();
+      const std::pair<uint32_t, uint64_t> b = rem[--top[pick]];
       kern::ScoreTask t{};
       t.begin = a.second;
       t.count1 = r1;
@@ -158,22 +172,13 @@ inline size_t CountScoreTasks(uint64_t cand_begin, uint64_t n, uint32_t q_first,
 
 // The blocks BuildScoreTasksPaired would make, from a histogram of the
 // remainders (no tasks built).
-inline size_t CountPairedTasks(uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32_t q_end,
-                               const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets,
-                               uint32_t per_block) {
-  std::vector<uint64_t> rem(per_block, 0);
+// Blocks the pairing makes from a histogram of remainder sizes (rem[r] =
+// remainders of size r; rem[0] ignored): BuildScoreTasksPaired's greedy in
+// batches, every remainder of size r1 taking the same partner size while
+// partners of that size last.
+inline size_t PairedFromRemainders(std::vector<uint64_t> rem, uint32_t per_block) {
   size_t nt = 0;
-  const uint64_t cand_end = cand_begin + n;
-  for (uint32_t qi = q_first; qi < q_end; ++qi) {
-    const uint64_t lo = std::max<uint64_t>(offsets[qi], cand_begin);
-    const uint64_t hi = std::min<uint64_t>(offsets[qi] + counts[qi], cand_end);
-    if (lo >= hi) continue;
-    nt += (hi - lo) / per_block;
-    ++rem[(hi - lo) % per_block];
-  }
   rem[0] = 0;
-  // BuildScoreTasksPaired's greedy in batches: every remainder of size r1 takes
-  // the same partner size while partners of that size last
   for (uint32_t r1 = per_block - 1; r1 >= 1; --r1) {
     while (rem[r1]) {
       uint32_t r2 = std::min(r1, per_block - r1);
@@ -196,6 +201,68 @@ inline size_t CountPairedTasks(uint64_t cand_begin, uint64_t n, uint32_t q_first
   return nt;
 }
 
+// The blocks BuildScoreTasksPaired would make (no tasks built).
+inline size_t CountPairedTasks(uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32_t q_end,
+                               const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets,
+                               uint32_t per_block) {
+  std::vector<uint64_t> rem(per_block, 0);
+  size_t full = 0;
+  const uint64_t cand_end = cand_begin + n;
+  for (uint32_t qi = q_first; qi < q_end; ++qi) {
+    const uint64_t lo = std::max<uint64_t>(offsets[qi], cand_begin);
+    const uint64_t hi = std::min<uint64_t>(offsets[qi] + counts[qi], cand_end);
+    if (lo >= hi) continue;
+    full += (hi - lo) / per_block;
+    ++rem[(hi - lo) % per_block];
+  }
+  return full + PairedFromRemainders(std::move(rem), per_block);
+}
+
+// The three block counts the chooser compares, in one pass over the queries:
+// consecutive runs of two and of four queries (CountScoreTasks) and the pairs
+// (CountPairedTasks).
+inline void CountTasks(uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32_t q_end,
+                       const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets, uint32_t per_block,
+                       size_t *n2, size_t *n4, size_t *np) {
+  struct Runs {
+    uint32_t qmax, cur = 0, open_q = 0;
+    bool open = false;
+    size_t nt = 0;
+    void Add(uint32_t qi, uint64_t len, uint32_t per_block) {
+      while (len) {
+        if (open && (cur == per_block || qi - open_q >= qmax)) {
+          ++nt;
+          open = false;
+        }
+        if (!open) {
+          cur = 0;
+          open_q = qi;
+          open = true;
+        }
+        const uint64_t take = std::min<uint64_t>(len, per_block - cur);
+        cur += (uint32_t)take;
+        len -= take;
+      }
+    }
+    size_t Done() const { return nt + (open && cur ? 1 : 0); }
+  } two{kern::kScoreQmaxUnit}, four{kern::kScoreQmax};
+  std::vector<uint64_t> rem(per_block, 0);
+  size_t full = 0;
+  const uint64_t cand_end = cand_begin + n;
+  for (uint32_t qi = q_first; qi < q_end; ++qi) {
+    const uint64_t lo = std::max<uint64_t>(offsets[qi], cand_begin);
+    const uint64_t hi = std::min<uint64_t>(offsets[qi] + counts[qi], cand_end);
+    if (lo >= hi) continue;
+    two.Add(qi, hi - lo, per_block);
+    four.Add(qi, hi - lo, per_block);
+    full += (hi - lo) / per_block;
+    ++rem[(hi - lo) % per_block];
+  }
+  *n2 = two.Done();
+  *n4 = four.Done();
+  *np = full + PairedFromRemainders(rem, per_block);
+}
+
 // The K2 tasks of a segment, and which kernel runs them (GHOSTM_K2=unit|swar16
 // and GHOSTM_K2_TASKS=paired|consecutive force a choice). With 16-bit integer
 // patterns (swar) the unit-pair kernel is used where its blocks, each ~7 %
@@ -214,13 +281,16 @@ inline size_t BuildTasks(bool swar, uint64_t cand_begin, uint64_t n, uint32_t q_
   const char *how = getenv("GHOSTM_K2_TASKS");
   const bool force_unit = k2 && strcmp(k2, "unit") == 0, force_rows = k2 && strcmp(k2, "swar16") == 0;
   bool unit = false, paired = false;
-  if (swar && q_end > q_first && !force_rows) {
-    const size_t nc = CountScoreTasks(cand_begin, n, q_first, q_end, counts, offsets, per_block,
-                                      kern::kScoreQmaxUnit);
-    const size_t np = CountPairedTasks(cand_begin, n, q_first, q_end, counts, offsets, per_block);
+  const uint64_t per_query = n / std::max<uint32_t>(1, q_end - q_first);
+  if (swar && q_end > q_first && !force_rows && !how && !force_unit && per_query >= 96) {
+    unit = true;  // dense (cfg 4: 127 per query): runs of two queries fill their blocks, no count needed
+  } else if (swar && q_end > q_first && !force_rows && (how || force_unit || per_query >= 24)) {
+    // (the count is on the critical path of a chunk's first segment: ~0.5 ms
+    // per 125 K queries; below 24 per query the rows kernel always won)
+    size_t nc, n4, np;
+    CountTasks(cand_begin, n, q_first, q_end, counts, offsets, per_block, &nc, &n4, &np);
     paired = how ? strcmp(how, "paired") == 0 : np * 100 <= nc * 95;
     const size_t nu = paired ? np : nc;
-    const size_t n4 = CountScoreTasks(cand_begin, n, q_first, q_end, counts, offsets, per_block, kern::kScoreQmax);
     unit = force_unit || nu * 100 <= n4 * 107;
     if (getenv("GHOSTM_DEBUG_TASKS"))
       fprintf(stderr, "k2 tasks: %llu candidates, %u queries: consecutive(2) %zu, paired %zu, consecutive(4) %zu -> %s\n",

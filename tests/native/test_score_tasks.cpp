@@ -95,6 +95,16 @@ int main() {
           return 1;
         }
       } else {
+        {
+          size_t c2, c4, cp;
+          ghostm::CountTasks(b, n, q0, q1, counts, offsets, per_block, &c2, &c4, &cp);
+          if (c2 != ghostm::CountScoreTasks(b, n, q0, q1, counts, offsets, per_block, 2) ||
+              c4 != ghostm::CountScoreTasks(b, n, q0, q1, counts, offsets, per_block, 4) ||
+              cp != ghostm::CountPairedTasks(b, n, q0, q1, counts, offsets, per_block)) {
+            printf("CountTasks disagrees with the single counters\n");
+            return 1;
+          }
+        }
         what = "chosen kernel";
         bool unit_k = false;
         nt = ghostm::BuildTasks(true, b, n, q0, q1, counts, offsets, per_block, tasks.data(), &unit_k);

@@ -1,0 +1,9 @@
+# round 4: host timelines of one cfg3 step, this build and the round-3 library
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+mkdir -p gpurun_out/r4r /tmp/tr3
+for v in cur r3 cur r3; do
+  L=$R/ghostm_amd/lib/libghostm_hip.so; [ $v = r3 ] && L=$R/ghostm_amd/lib/libghostm_hip_r3.so
+  GHOSTM_LIB_PATH=$L GHOSTM_TRACE=1 timeout -k 10 200 python3 bench.py --preset cfg3 --steps 3 --warmup 1 --no-cpu --no-e2e --workdir /tmp/tr3 > gpurun_out/r4r/$v.json 2> gpurun_out/r4r/$v.log || exit $?
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1].split('/')[-1], round(d['ms_per_step'],2))" gpurun_out/r4r/$v.json
+done
