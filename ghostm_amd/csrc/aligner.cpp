@@ -1403,7 +1403,9 @@ void Session::Run(bool stream_to_file) {
   hits_.clear();
   hits_valid_ = false;
   Format();  // built here, before any formatting task can need it
-  dev.ResetRecords();
+  uint64_t expect = 0;  // the most records the run can append: each group keeps -b hits
+  for (const QueryData &q : queries_) expect += (uint64_t)q.group_first.size() * std::max<uint32_t>(opt_.best, 1);
+  dev.ResetRecords(expect);
   records_on_device_ = true;
   const double t0 = NowSeconds();
   TraceMark("run");

@@ -176,7 +176,10 @@ class DeviceModule {
   // Device-resident hit records of the current run (GhostmHit layout, 32 B),
   // for the multi-GPU gather. AppendRecords turns the last MergeSelect's hits
   // (groups [g0, g0 + counts.size())) into records at the end of the array.
-  void ResetRecords();
+  // expect: the run's record bound (its groups x -b), reserved up front so
+  // the array does not grow (reallocate and free) while the run's kernels are
+  // queued; at most kRecordReserveMax bytes, beyond that it grows on demand
+  void ResetRecords(uint64_t expect = 0);
   void AppendRecords(DevQuery *q, uint32_t g0, const std::vector<uint32_t> &counts, uint32_t cap,
                      uint32_t q_base, bool from_carry = false);  // from_carry: groups' carried lists
   void UploadRecords(const void *records, uint64_t n);  // host records (other paths)

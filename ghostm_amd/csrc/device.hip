@@ -38,6 +38,7 @@ struct PinnedBuf {
     if (p) HIP_CHECK(hipHostFree(p));
     p = nullptr;
     bytes = 0;
+    if (TraceOn()) TraceMark("pin_alloc", b);
     HIP_CHECK(hipHostMalloc(&p, std::max<size_t>(b, 256), hipHostMallocDefault));
     bytes = std::max<size_t>(b, 256);
   }
@@ -53,10 +54,12 @@ struct DevBuf {
     p = nullptr;
     bytes = 0;
     size_t want = std::max<size_t>(b, 256);
+    if (TraceOn()) TraceMark("dev_alloc", want);
     HIP_CHECK(hipMalloc(&p, want));
     bytes = want;
   }
   void Release() {
+    if (p && TraceOn()) TraceMark("dev_free", bytes);
     if (p) (void)hipFree(p);
     p = nullptr;
     bytes = 0;
@@ -590,6 +593,11 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
   I.list_beg.Reserve((size_t)nq * nlists * 4);
   I.list_len.Reserve((size_t)nq * nlists * 4);
   SettleSeedTime();
+  if (TraceOn()) {  // timeline only: is the stream idle before K1 starts?
+    HIP_CHECK(hipEventRecord(I.ev_nb, S(stream_)));
+    HIP_CHECK(hipEventSynchronize(I.ev_nb));
+    TraceMark("k1_idle");
+  }
   HIP_CHECK(hipEventRecord(I.ev_s0, S(stream_)));
   HIP_CHECK(hipMemsetAsync(I.counts.p, 0, (size_t)nq * 4, S(stream_)));
   TraceMark("k1a_memset");
@@ -1484,8 +1492,6 @@ void DeviceModule::MergeSelect(DevQuery *q, DevDb *d, uint32_t g0, uint32_t g1, 
   MergeCollect(counts, hits);
 }
 
-void DeviceModule::ResetRecords() { records_ = 0; }
-
 static void GrowRecords(DevBuf &buf, uint64_t records, uint64_t want, hipStream_t st) {
   const size_t need = (size_t)want * sizeof(kern::HitRecord32);
   if (need <= buf.bytes) return;
@@ -1498,6 +1504,16 @@ static void GrowRecords(DevBuf &buf, uint64_t records, uint64_t want, hipStream_
   buf = bigger;
   bigger.p = nullptr;
   bigger.bytes = 0;
+}
+
+static constexpr uint64_t kRecordReserveMax = 8ull << 30;
+
+void DeviceModule::ResetRecords(uint64_t expect) {
+  records_ = 0;
+  if (!impl_ || !expect) return;
+  Use();
+  expect = std::min<uint64_t>(expect, kRecordReserveMax / sizeof(kern::HitRecord32));
+  GrowRecords(impl_->records, 0, expect, S(stream_));
 }
 
 void DeviceModule::AppendRecords(DevQuery *q, uint32_t g0, const std::vector<uint32_t> &counts, uint32_t cap,
