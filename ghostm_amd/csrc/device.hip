@@ -197,6 +197,7 @@ constexpr size_t kFilterLds2 = (131072 / 16 + 9216 + 6144) * 4;
 
 // K3a: the pair table (32 x 32 codes x 32 query codes, one word each) + histogram
 static constexpr size_t kScanLds = (size_t)kern::kPairWords * 4 + kern::kSortBins * 4;
+static constexpr size_t kScanLdsPriv = (size_t)kern::kPrivWords * 4 + kern::kSortBins * 4;  // GHOSTM_K3_SCAN=priv
 
 // Host landing of a segment's selected hits (HostHits): a fresh, uninitialised
 // heap block per segment, freed by the formatter when it is done with it.
@@ -283,6 +284,12 @@ void DeviceModule::Bind(int device) {
   GHOSTM_SCAN_ATTRW(32, true) GHOSTM_SCAN_ATTRW(32, false) GHOSTM_SCAN_ATTRW(16, true)
   GHOSTM_SCAN_ATTRW(16, false) GHOSTM_SCAN_ATTRW(8, true) GHOSTM_SCAN_ATTRW(8, false)
 #undef GHOSTM_SCAN_ATTRW
+#define GHOSTM_SCAN_ATTRP(SS, EE)                                                            \
+  HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_tb_scan<SS, true, EE, true, true, true>, \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kScanLdsPriv));
+  GHOSTM_SCAN_ATTRP(32, true) GHOSTM_SCAN_ATTRP(32, false) GHOSTM_SCAN_ATTRP(16, true)
+  GHOSTM_SCAN_ATTRP(16, false) GHOSTM_SCAN_ATTRP(8, true) GHOSTM_SCAN_ATTRP(8, false)
+#undef GHOSTM_SCAN_ATTRP
 #undef GHOSTM_SCAN_ATTR2
 #undef GHOSTM_SCAN_ATTR
   {
@@ -1243,8 +1250,15 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
 #define GHOSTM_SCANW(SS, EE)                                                                                  \
   hipLaunchKernelGGL((kern::k_tb_scan<SS, true, EE, true, true>), dim3(blocks), dim3(kern::kScanBlock), kScanLds, \
                      S(stream_), sa)
+#define GHOSTM_SCANP(SS, EE)                                                                                      \
+  hipLaunchKernelGGL((kern::k_tb_scan<SS, true, EE, true, true, true>), dim3(blocks), dim3(kern::kScanBlock), \
+                     kScanLdsPriv, S(stream_), sa)
+    // GHOSTM_K3_SCAN=priv: the bank-private table (A/B)
+    const bool priv = swar && scan_env && strcmp(scan_env, "priv") == 0;
 #define GHOSTM_SCAN(SS)                                          \
-  if (swar && exact) GHOSTM_SCANW(SS, true);                     \
+  if (priv && exact) GHOSTM_SCANP(SS, true);                     \
+  else if (priv) GHOSTM_SCANP(SS, false);                        \
+  else if (swar && exact) GHOSTM_SCANW(SS, true);                \
   else if (swar) GHOSTM_SCANW(SS, false);                        \
   else if (framed && exact) GHOSTM_SCAN1(SS, true, true, true);  \
   else if (framed) GHOSTM_SCAN1(SS, true, false, true);          \
@@ -1258,6 +1272,7 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
       default: GHOSTM_SCAN(8); break;
     }
 #undef GHOSTM_SCAN
+#undef GHOSTM_SCANP
 #undef GHOSTM_SCANW
 #undef GHOSTM_SCAN1
     hipLaunchKernelGGL(kern::k_csort_scatter, gsort, b256, 0, S(stream_), I.tb_skey.as<uint32_t>(), n, false,

@@ -26,6 +26,7 @@
 
 #include "libstdcxx_sort.h"
 #include "score_task.h"
+#include "seed_lists.h"
 
 namespace ghostm {
 namespace kern {
@@ -590,6 +591,24 @@ __global__ __launch_bounds__(BLOCK) void k_seed_hash(SeedArgs a) {
   EmitFromTable<BLOCK, TSLOTS>(a, q, s_tab, s_emit, s_part, &s_total);
 }
 
+#ifndef GHOSTM_K1_PREFETCH
+#define GHOSTM_K1_PREFETCH 0
+#endif
+#ifndef GHOSTM_K1_GUARD  // A/B: 0 runs every entry slot of the wave's chunks
+#define GHOSTM_K1_GUARD 1
+#endif
+// Diagnostics builds (-DGHOSTM_K1_STOP=N, tools/altlib.sh): k_seed_filter ends
+// after phase N with no candidates, to time its phases. Never in the product.
+#ifdef GHOSTM_K1_STOP
+#define GHOSTM_K1_PHASE_END(N)                   \
+  if constexpr (GHOSTM_K1_STOP == (N)) {         \
+    if (tid == 0) a.counts[q] = 0;               \
+    return;                                      \
+  }
+#else
+#define GHOSTM_K1_PHASE_END(N)
+#endif
+
 // K1b'' k_seed_filter<BLOCK, FSLOTS, TSLOTS, QCAP>: k_seed_hash's exact table
 //     behind a presence filter, for thresholds >= 2. Most (list, bin) entries of
 //     a query are lone k-mer hits that can never be emitted: bin b is emitted
@@ -650,9 +669,10 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   const uint32_t n = s_off[nl];
 
   // 0. the list of every entry, one byte each, in the queue's LDS (dead until
-  //    pass 2): thread t finds the list of entry 16 t once (the chunk's first
-  //    list, then the boundaries up to it) and walks its 16 entries, so pass 1
-  //    reads an entry's list with one ds_read_u8 instead of a search per entry
+  //    pass 2): thread t finds the list j0 of entry 16 t once (the chunk's
+  //    first list, then the boundaries up to it) and fills its 16 bytes from
+  //    the list boundaries inside its window (ListBytes16, seed_lists.h), so
+  //    pass 1 reads an entry's list with one ds_read_u8
   static_assert(QCAP * 4 >= 16 * BLOCK && 16 * BLOCK >= 64 * KE * kW, "entry list bytes alias the queue");
   uint8_t *const s_lst = reinterpret_cast<uint8_t *>(s_q);
   {
@@ -661,22 +681,106 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
     if (e0 < n) {
       uint32_t j = s_cfirst[e0 >> 6];
       while (s_off[j + 1] <= e0) ++j;
-      uint32_t nxt = s_off[j + 1];
-#pragma unroll
-      for (uint32_t k = 0; k < 16; ++k) {
-        while (e0 + k >= nxt && j + 1 < nl) nxt = s_off[++j + 1];  // (empty lists: several steps)
-        wv[k >> 2] |= j << (8 * (k & 3));
-      }
+      ListBytes16(e0, j, s_off, nl, wv);
     }
     reinterpret_cast<uint4 *>(s_lst)[tid] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
   }
   __syncthreads();
+  GHOSTM_K1_PHASE_END(1);
 
   // 1. gather: chunk c = wave + kW * e (64 entries of the concatenated lists),
-  //    lane = entry within the chunk; bins stay in registers
+  //    lane = entry within the chunk; bins stay in registers. The wave's
+  //    chunks past n (e >= ne, wave-uniform) are skipped by scalar branches.
+  const uint32_t nch = (n + 63) >> 6;
+  const uint32_t ne =
+      GHOSTM_K1_GUARD ? __builtin_amdgcn_readfirstlane(nch > wave ? min(KE, (nch - wave + kW - 1) / kW) : 0u) : KE;
+#if GHOSTM_K1_PREFETCH  // A/B variant (tools/altlib.sh -DGHOSTM_K1_PREFETCH=1)
+  // every chunk's positions are requested before any is used (one exposure of
+  // the gather latency per wave instead of one per four chunks)
+  uint32_t pos[KE], prv[KE], lst[KE];
+#pragma unroll
+  for (uint32_t e0 = 0; e0 < KE; e0 += 4) {
+    if (e0 >= ne) {
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u) {
+        pos[e0 + u] = 0;
+        prv[e0 + u] = kNone;
+        lst[e0 + u] = kNone;
+      }
+      continue;
+    }
+    uint32_t ii[4], jj[4], dd[4];
+    // the four entries' list bytes, then their position offsets, as two batches
+    // of LDS reads (every entry index stays inside the byte table)
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) {
+      ii[u] = ((wave + kW * (e0 + u)) << 6) + lane;
+      jj[u] = s_lst[ii[u]];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) dd[u] = s_delta[jj[u]];
+    // (kept here: the compiler otherwise sinks both reads into each entry's
+    // branch below and waits for them one entry at a time)
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) asm volatile("" : "+v"(dd[u]));
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) {
+      const uint32_t i = ii[u], j = jj[u];
+      pos[e0 + u] = 0;
+      prv[e0 + u] = kNone;
+      lst[e0 + u] = kNone;
+      if (i < n) {
+        const uint32_t at = i + dd[u];  // = list_beg[j] + (i - s_off[j])
+        pos[e0 + u] = a.positions[at];
+        lst[e0 + u] = j;
+        if (lane == 0 && i != s_off[j]) prv[e0 + u] = a.positions[at - 1];
+      }
+    }
+  }
+  // bins, the duplicate test, and the filter marks: four entries' marks are
+  // issued before the first is read back (the seen-twice mark needs the old word)
   uint32_t bin[KE];
 #pragma unroll
   for (uint32_t e0 = 0; e0 < KE; e0 += 4) {
+    if (e0 >= ne) {
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u) bin[e0 + u] = kNone;
+      continue;
+    }
+    uint32_t fw[4], fb[4], old[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) {
+      const uint32_t j = lst[e0 + u];
+      const uint32_t pj = ShiftUp(j), pp = ShiftUp(pos[e0 + u]);
+      uint32_t prev_pos = prv[e0 + u];
+      if (lane > 0 && pj == j) prev_pos = pp;
+      uint32_t x = kNone;
+      if (j != kNone) {
+        const uint32_t d0 = __umul24(j, a.shift);  // j < 128: full-rate 24-bit multiply
+        const uint32_t b = (pos[e0 + u] - d0) >> a.log_region;
+        const bool dup = prev_pos != kNone && ((prev_pos - d0) >> a.log_region) == b;
+        if (!dup) x = b;
+      }
+      bin[e0 + u] = x;
+      const uint32_t cell = x & (FSLOTS - 1);
+      fw[u] = cell >> 4;
+      fb[u] = x != kNone ? 1u << ((cell & 15) * 2) : 0u;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) old[u] = fb[u] ? atomicOr(&s_flt[fw[u]], fb[u]) : 0u;
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u)
+      if (old[u] & fb[u]) atomicOr(&s_flt[fw[u]], fb[u] << 1);
+  }
+#else
+  uint32_t bin[KE];
+#pragma unroll
+  for (uint32_t e0 = 0; e0 < KE; e0 += 4) {
+    if (e0 >= ne) {
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u) bin[e0 + u] = kNone;
+      continue;
+    }
     uint32_t pos[4], prv[4], lst[4], ii[4], jj[4], dd[4];
     // the four entries' list bytes, then their position offsets, as two batches
     // of LDS reads (every entry index stays inside the byte table)
@@ -725,7 +829,9 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
       bin[e0 + u] = x;
     }
   }
+#endif
   __syncthreads();
+  GHOSTM_K1_PHASE_END(2);
 
   // 2. filter, then per-wave compaction into the queue
   //    cells x - 1, x, x + 1 in bits 0-5 from the words holding x - 1 and
@@ -738,6 +844,8 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   unsigned long long bal[KE];  // wave-uniform: SGPR pairs
 #pragma unroll
   for (uint32_t e = 0; e < KE; ++e) {
+    bal[e] = 0;
+    if (e >= ne) continue;
     const uint32_t x = bin[e];
     bool nd = false;
     if (x != kNone) nd = x <= 1 || (near(x) & 0x19u) != 0;  // seen(x - 1), twice(x), seen(x + 1)
@@ -749,6 +857,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   qbase = (uint32_t)__shfl((int)qbase, 0);
 #pragma unroll
   for (uint32_t e = 0; e < KE; ++e) {
+    if (e >= ne) continue;
     const unsigned long long m = bal[e];
     const bool nd = (m >> lane) & 1ull;
     const uint32_t at = qbase + (uint32_t)__popcll(m & ((1ull << lane) - 1));
@@ -761,6 +870,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
     if (tid == 0) a.counts[q] = kOverflow;
     return;
   }
+  GHOSTM_K1_PHASE_END(3);
 
   // 3. exact counts of the kept entries; the lane whose insert created a
   //    bin's slot remembers it, so step 4 visits each occupied slot once with
@@ -775,6 +885,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
     made[u] = k < qn ? table.Insert(s_q[k]) : kNone;
   }
   __syncthreads();
+  GHOSTM_K1_PHASE_END(4);
 
   // 4. emission rule per created slot, as EmitFromTable
   const uint32_t thr = a.threshold;
@@ -2607,6 +2718,12 @@ constexpr uint32_t kPairCodes = 26;    // DB codes 0..25 (25 = END) index the pa
 // bank q: 20 amino-acid codes among a wave's 32 lanes of one ds_read_b32 group)
 constexpr uint32_t kPairStride = 33;
 constexpr uint32_t kPairWords = kPairCodes * kPairCodes * kPairStride;
+// PRIV scan table (GHOSTM_K3_SCAN=priv): one unit word (v, 1) per (DB code,
+// query code), 32 copies interleaved dword by dword so that lane l reads only
+// bank l mod 32 (no conflicts). A row reads hit A's word and hit B's word, and
+// one op_sel v_pk_mad_u16 adds both values to H (K2's unit-pair sum).
+constexpr uint32_t kPrivColBytes = 32 * 32 * 4;                // one DB code: 32 query codes x 32 banks
+constexpr uint32_t kPrivWords = kPairCodes * 32 * 32;          // 106 KB
 
 // Per slot: the reverse window (0 = empty slot; counted into *empty), ncols
 // reset to 0.
@@ -2837,15 +2954,24 @@ __global__ void k_rev_codes(const uint8_t *qseq, uint32_t nq, uint32_t L, uint32
 // the oE and F steps: three of the six packed ops per row pair become VOP2 adds
 // (every value, dead halves included, stays in [64, 0x7C00): no carry crosses
 // the halves, and the packed f16 maxima order the patterns as integers).
-template <int S, bool HALF, bool EXACT, bool FRAMED = false, bool SWAR = false>
+template <int S, bool HALF, bool EXACT, bool FRAMED = false, bool SWAR = false, bool PRIV = false>
 __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
   using C = Cells<HALF>;
   static_assert(!FRAMED || HALF, "the frame is an f16 kernel");
   static_assert(!SWAR || FRAMED, "integer patterns: the framed kernel");
+  static_assert(!PRIV || SWAR, "the bank-private table: the integer-pattern scan");
   extern __shared__ __attribute__((aligned(16))) uint32_t s_pair[];
-  uint32_t *s_hist = s_pair + kPairWords;
+  uint32_t *s_hist = s_pair + (PRIV ? kPrivWords : kPairWords);
   const int extp = -a.ext;
-  for (uint32_t e = threadIdx.x; e < kPairWords; e += kScanBlock) {
+  if constexpr (PRIV) {
+    for (uint32_t e = threadIdx.x; e < kPrivWords; e += kScanBlock) {
+      const uint32_t d = e >> 5, ca = d >> 5, q = d & 31;  // (DB code, query code)
+      const int m = ca < 25 && q < 25 ? a.mat[ca * 32 + q] : 0;
+      const int v = (q == kPadCode || ca == kSeqEnd) ? 64 - (int)a.swar_low : m + extp;
+      s_pair[e] = (uint32_t)(uint16_t)v | 0x10000u;
+    }
+  }
+  for (uint32_t e = threadIdx.x; e < (PRIV ? 0u : kPairWords); e += kScanBlock) {
     const uint32_t pr = e / kPairStride, q = e - pr * kPairStride;
     const uint32_t ca = pr / kPairCodes, cb = pr - ca * kPairCodes;
     int va = q == kPadCode ? kNeg16 : (ca < 25 && q < 25 ? a.mat[ca * 32 + q] : 0);
@@ -2901,6 +3027,16 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
         const uint2 v = *reinterpret_cast<const uint2 *>(rw);  // S = 8: two words
         qoff[0] = v.x;
         qoff[1] = v.y;
+      }
+    }
+    // PRIV: each row's byte offset in the bank-private table (query code part
+    // plus this lane's bank); the column adds its DB code's part
+    uint32_t rp[PRIV ? S : 1];
+    if constexpr (PRIV) {
+#pragma unroll
+      for (int u = 0; u < S; ++u) {
+        const uint32_t qc = ((qoff[u >> 2] >> (8 * (u & 3))) & 0xFFu) >> 2;
+        rp[u] = qc * 128u + (lane & 31u) * 4u;
       }
     }
     uint32_t H[S], E[S];
@@ -2979,27 +3115,38 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
       const hf2 Z1 = SWAR ? HF(sig + EXTP) : HF(W(HF(sig) + HF(EXTP)));  // FRAMED: the next column's frame
       const hf2 KOE = HF(Cells<true>::Pair(a.open - a.ext)), NEXT = HF(Cells<true>::Pair(a.ext));
       const char *tp = reinterpret_cast<const char *>(s_pair) + cbase;
-      auto T = [&](int u) { return *reinterpret_cast<const uint32_t *>(tp + ((qoff[u >> 2] >> (8 * (u & 3))) & 0xFFu)); };
+      const char *tpa = reinterpret_cast<const char *>(s_pair) + min(rA, kPairCodes - 1) * kPrivColBytes;
+      const char *tpb = reinterpret_cast<const char *>(s_pair) + min(rB, kPairCodes - 1) * kPrivColBytes;
+      using TW = std::conditional_t<PRIV, uint2, uint32_t>;
+      auto T = [&](int u) -> TW {
+        if constexpr (PRIV) {
+          return make_uint2(*reinterpret_cast<const uint32_t *>(tpa + rp[u]),
+                            *reinterpret_cast<const uint32_t *>(tpb + rp[u]));
+        } else {
+          return *reinterpret_cast<const uint32_t *>(tp + ((qoff[u >> 2] >> (8 * (u & 3))) & 0xFFu));
+        }
+      };
       uint32_t diag = diag0, F = fin, cm = sig;
       if constexpr (FRAMED) {
         // software-pipelined by chunks of eight rows: the next chunk's eight
         // table reads are issued before this chunk's rows, and each row's
         // diagonal sum is formed one row ahead, from the old H just before the
         // row above overwrites it
-        constexpr int CH = 8;
+        constexpr int CH = PRIV ? 4 : 8;  // PRIV: two words per row, half the rows ahead
         // two read-ahead sets used in turn by chunk parity (a fixed register
         // set per chunk after unrolling: no copies of the next chunk's reads)
-        uint32_t tt[2][CH];
+        TW tt[2][CH];
 #pragma unroll
         for (int u = 0; u < CH; ++u) tt[0][u] = T(u);
-        auto dsum = [](uint32_t h, uint32_t tv) -> uint32_t {
-          if constexpr (SWAR) return h + tv;  // v_add_u32 over both halves
+        auto dsum = [](uint32_t h, TW tv) -> uint32_t {
+          if constexpr (PRIV) return PkMadUnit(tv.x, tv.y, h);  // (vA, 1), (vB, 1): one v_pk_mad_u16
+          else if constexpr (SWAR) return h + tv;  // v_add_u32 over both halves
           else return W(HF(h) + HF(tv));
         };
         uint32_t sc = dsum(diag, tt[0][0]);
 #pragma unroll
         for (int k = 0; k < S; k += CH) {
-          uint32_t *t = tt[(k / CH) & 1], *tn = tt[((k / CH) & 1) ^ 1];
+          TW *t = tt[(k / CH) & 1], *tn = tt[((k / CH) & 1) ^ 1];
           if (k + CH < S) {
 #pragma unroll
             for (int u = 0; u < CH; ++u) tn[u] = T(k + CH + u);
