@@ -189,10 +189,17 @@ static constexpr uint32_t kSlotCap = 256;
 // Filtered slot pass (k_seed_filter) of classes 0, 1 and 2, thresholds >= 2:
 // <BLOCK, filter cells, table slots, queue> and its dynamic LDS bytes.
 #define GHOSTM_FILTER0 kern::k_seed_filter<256, 32768, 2304, 1536>
-#define GHOSTM_FILTER1 kern::k_seed_filter<512, 65536, 4608, 3072>
+#ifndef GHOSTM_K1_F1SLOTS  // class 1's filter cells (A/B builds: tools/altlib.sh -DGHOSTM_K1_F1SLOTS=131072)
+#define GHOSTM_K1_F1SLOTS 65536
+#endif
+#ifndef GHOSTM_K1_F1ALIAS  // class 1's bitmap sharing the exact table's LDS (A/B)
+#define GHOSTM_K1_F1ALIAS false
+#endif
+#define GHOSTM_FILTER1 kern::k_seed_filter<512, GHOSTM_K1_F1SLOTS, 4608, 3072, GHOSTM_K1_F1ALIAS>
 #define GHOSTM_FILTER2 kern::k_seed_filter<1024, 131072, 9216, 6144>
 constexpr size_t kFilterLds0 = (32768 / 16 + 2304 + 1536) * 4;
-constexpr size_t kFilterLds1 = (65536 / 16 + 4608 + 3072) * 4;
+constexpr size_t kFilterLds1 =
+    ((GHOSTM_K1_F1ALIAS ? std::max<size_t>(GHOSTM_K1_F1SLOTS / 16, 4608) : GHOSTM_K1_F1SLOTS / 16 + 4608) + 3072) * 4;
 constexpr size_t kFilterLds2 = (131072 / 16 + 9216 + 6144) * 4;
 
 // K3a: the pair table (32 x 32 codes x 32 query codes, one word each) + histogram

@@ -624,13 +624,18 @@ __global__ __launch_bounds__(BLOCK) void k_seed_hash(SeedArgs a) {
 //     emission is k_seed_hash's: every occupied bin and its b + 1 neighbour
 //     have exact counts, so the emitted set and order are identical. A query
 //     whose queue exceeds QCAP is marked kOverflow and redone by k_seed_hash.
-template <uint32_t BLOCK, uint32_t FSLOTS, uint32_t TSLOTS, uint32_t QCAP>
+// ALIAS: the filter bitmap and the exact table share one region (the bitmap is
+// dead once pass 2 has compacted the queue, the table unused before pass 3),
+// so a larger bitmap (fewer aliased cells, fewer entries queued) fits the same
+// LDS; the table is zeroed after pass 2 instead of with the bitmap.
+template <uint32_t BLOCK, uint32_t FSLOTS, uint32_t TSLOTS, uint32_t QCAP, bool ALIAS = false>
 __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
   constexpr uint32_t kFWords = FSLOTS / 16;   // 16 two-bit cells per word
+  constexpr uint32_t kRegion = ALIAS ? (kFWords > TSLOTS ? kFWords : TSLOTS) : kFWords + TSLOTS;
   uint32_t *const s_flt = s_dyn;
-  uint32_t *const s_tab = s_dyn + kFWords;
-  uint32_t *const s_q = s_tab + TSLOTS;
+  uint32_t *const s_tab = ALIAS ? s_dyn : s_dyn + kFWords;
+  uint32_t *const s_q = s_dyn + kRegion;
   constexpr uint32_t kW = BLOCK / 64;
   constexpr uint32_t KE = 16;                 // entries per lane: n <= 64 * KE * kW
   constexpr uint32_t kChunks = KE * kW;
@@ -650,7 +655,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   // filter bitmap and exact table zeroed with 16-byte stores (both are
   // multiples of four words, s_dyn 16-byte aligned)
   static_assert(kFWords % 4 == 0 && TSLOTS % 4 == 0, "16-byte zeroing");
-  for (uint32_t k = tid; k < (kFWords + TSLOTS) / 4; k += BLOCK)
+  for (uint32_t k = tid; k < (ALIAS ? kFWords : kFWords + TSLOTS) / 4; k += BLOCK)
     reinterpret_cast<uint4 *>(s_dyn)[k] = make_uint4(0u, 0u, 0u, 0u);
   if (tid == 0) s_qn = 0;
   uint32_t len = 0, beg = 0;
@@ -869,6 +874,10 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   if (qn > QCAP) {  // block-uniform: redone by k_seed_hash
     if (tid == 0) a.counts[q] = kOverflow;
     return;
+  }
+  if constexpr (ALIAS) {  // the bitmap is dead: the exact table takes its place
+    for (uint32_t k = tid; k < TSLOTS / 4; k += BLOCK) reinterpret_cast<uint4 *>(s_tab)[k] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
   }
   GHOSTM_K1_PHASE_END(3);
 

@@ -4,9 +4,9 @@
 #include <cstdint>
 
 #if defined(__HIPCC__)
-#define GHOSTM_HD __host__ __device__
+#define GHOSTM_SEED_HD __host__ __device__
 #else
-#define GHOSTM_HD
+#define GHOSTM_SEED_HD
 #endif
 
 namespace ghostm {
@@ -20,7 +20,7 @@ namespace kern {
 // one to the bytes at and after it: a loop over the boundaries, usually none
 // or one, instead of a test per entry. Bytes past the last list keep its
 // index (entries >= off[nl] are never read).
-GHOSTM_HD inline void ListBytes16(uint32_t e0, uint32_t j, const uint32_t *off, uint32_t nl, uint32_t wv[4]) {
+GHOSTM_SEED_HD inline void ListBytes16(uint32_t e0, uint32_t j, const uint32_t *off, uint32_t nl, uint32_t wv[4]) {
   const uint32_t fill = j * 0x01010101u;
   for (int w = 0; w < 4; ++w) wv[w] = fill;
   for (uint32_t nxt = off[j + 1]; nxt < e0 + 16 && j + 1 < nl; nxt = off[++j + 1]) {

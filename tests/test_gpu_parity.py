@@ -336,16 +336,16 @@ def test_wide_band_traceback_uses_key_kernel(dataset, golden, tmp_path):
     assert st["traceback_launches_key"] == st["traceback_launches"] > 0
 
 
-@pytest.mark.parametrize("mode", ["default", "f16frame", "f16plain", "int16", "0"])
+@pytest.mark.parametrize("mode", ["default", "priv", "f16frame", "f16plain", "int16", "0"])
 @pytest.mark.parametrize("ds,var,opts", [("syn_small", "default", []), ("syn_dna", "default", []),
                                          ("syn_chunks", "default", []), ("protein_testset", "y2", ["-y", "2"]),
                                          ("syn_small", "r64_pam250", ["-r", "64", "-M", cases.PAM250, "-y", "2"])])
 def test_traceback_scan_modes_match_golden(mode, ds, var, opts, dataset, golden, tmp_path):
     """Two-pass traceback (K3a scores-only scan, then the key DP over columns
     0..j* in j*-sorted order) in its encodings (default: the column-framed scan
-    over 16-bit integer patterns; f16frame, f16plain, int16), and the
-    single-pass traceback (GHOSTM_K3_SCAN=0):
-    each reproduces the golden output."""
+    over 16-bit integer patterns; priv: the same scan reading a bank-private
+    unit-word table; f16frame, f16plain, int16), and the single-pass traceback
+    (GHOSTM_K3_SCAN=0): each reproduces the golden output."""
     d = dataset(ds)
     env = {} if mode == "default" else {"GHOSTM_K3_SCAN": mode}
     text, st = _gpu_text(d, opts, env, str(tmp_path / "g.out"))
@@ -356,7 +356,8 @@ def test_traceback_scan_modes_match_golden(mode, ds, var, opts, dataset, golden,
         assert st["traceback_launches_scan"] == 0 and st["traceback_scan_cells"] == 0
     else:
         # default: the framed scan over 16-bit integer patterns; the others not
-        assert st["traceback_launches_scan_swar"] == (st["traceback_launches"] if mode == "default" else 0)
+        swar = mode in ("default", "priv")
+        assert st["traceback_launches_scan_swar"] == (st["traceback_launches"] if swar else 0)
         assert st["traceback_launches_scan"] == st["traceback_launches"]
         assert st["traceback_scan_cells"] > 0
         # the key DP runs only columns 0..j*: fewer cells than the scan covered
