@@ -187,20 +187,27 @@ struct DeviceModule::Impl {
 
 static constexpr uint32_t kSlotCap = 256;
 // Filtered slot pass (k_seed_filter) of classes 0, 1 and 2, thresholds >= 2:
-// <BLOCK, filter cells, table slots, queue> and its dynamic LDS bytes.
-#define GHOSTM_FILTER0 kern::k_seed_filter<256, 32768, 2304, 1536>
-#ifndef GHOSTM_K1_F1SLOTS  // class 1's filter cells (A/B builds: tools/altlib.sh -DGHOSTM_K1_F1SLOTS=131072)
-#define GHOSTM_K1_F1SLOTS 65536
+// <BLOCK, filter cells, table slots, queue, alias> and its dynamic LDS bytes.
+// The bitmap shares its LDS with the exact table (alias), which doubled the
+// cells each class can afford at the same occupancy: half the aliased cells,
+// so about half the lone entries that passed the filter only by aliasing are
+// no longer queued and counted (class 1, cfg4: 13.7 -> 11.4 ms per launch,
+// profiles/r4_k1/). GHOSTM_K1_ALIAS=0 builds the separate regions with the
+// earlier cell counts (A/B).
+#ifndef GHOSTM_K1_ALIAS
+#define GHOSTM_K1_ALIAS 1
 #endif
-#ifndef GHOSTM_K1_F1ALIAS  // class 1's bitmap sharing the exact table's LDS (A/B)
-#define GHOSTM_K1_F1ALIAS false
-#endif
-#define GHOSTM_FILTER1 kern::k_seed_filter<512, GHOSTM_K1_F1SLOTS, 4608, 3072, GHOSTM_K1_F1ALIAS>
-#define GHOSTM_FILTER2 kern::k_seed_filter<1024, 131072, 9216, 6144>
-constexpr size_t kFilterLds0 = (32768 / 16 + 2304 + 1536) * 4;
-constexpr size_t kFilterLds1 =
-    ((GHOSTM_K1_F1ALIAS ? std::max<size_t>(GHOSTM_K1_F1SLOTS / 16, 4608) : GHOSTM_K1_F1SLOTS / 16 + 4608) + 3072) * 4;
-constexpr size_t kFilterLds2 = (131072 / 16 + 9216 + 6144) * 4;
+constexpr bool kFilterAlias = GHOSTM_K1_ALIAS != 0;
+constexpr uint32_t kFilterScale = kFilterAlias ? 2 : 1;
+#define GHOSTM_FILTER0 kern::k_seed_filter<256, 32768 * kFilterScale, 2304, 1536, kFilterAlias>
+#define GHOSTM_FILTER1 kern::k_seed_filter<512, 65536 * kFilterScale, 4608, 3072, kFilterAlias>
+#define GHOSTM_FILTER2 kern::k_seed_filter<1024, 131072 * kFilterScale, 9216, 6144, kFilterAlias>
+constexpr size_t FilterLds(size_t cells, size_t table, size_t queue) {
+  return ((kFilterAlias ? std::max(cells / 16, table) : cells / 16 + table) + queue) * 4;
+}
+constexpr size_t kFilterLds0 = FilterLds(32768 * kFilterScale, 2304, 1536);
+constexpr size_t kFilterLds1 = FilterLds(65536 * kFilterScale, 4608, 3072);
+constexpr size_t kFilterLds2 = FilterLds(131072 * kFilterScale, 9216, 6144);
 
 // K3a: the pair table (32 x 32 codes x 32 query codes, one word each) + histogram
 static constexpr size_t kScanLds = (size_t)kern::kPairWords * 4 + kern::kSortBins * 4;

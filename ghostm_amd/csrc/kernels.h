@@ -594,8 +594,8 @@ __global__ __launch_bounds__(BLOCK) void k_seed_hash(SeedArgs a) {
 #ifndef GHOSTM_K1_PREFETCH
 #define GHOSTM_K1_PREFETCH 0
 #endif
-#ifndef GHOSTM_K1_GUARD  // A/B: 0 runs every entry slot of the wave's chunks
-#define GHOSTM_K1_GUARD 1
+#ifndef GHOSTM_K1_GUARD  // A/B: 1 skips the wave's chunk slots past n by scalar branches
+#define GHOSTM_K1_GUARD 0    // (measured slower: 13.42 against 13.14 ms per class-1 launch)
 #endif
 // Diagnostics builds (-DGHOSTM_K1_STOP=N, tools/altlib.sh): k_seed_filter ends
 // after phase N with no candidates, to time its phases. Never in the product.
