@@ -277,10 +277,19 @@ def main() -> None:
         backend = os.environ.get("GHOSTM_BENCH_BACKEND", "nccl")
         # a rank that never arrives ends the job instead of hanging it
         timeout = datetime.timedelta(seconds=float(os.environ.get("GHOSTM_BENCH_PG_TIMEOUT", "900")))
-        if backend == "nccl":
-            dist.init_process_group(backend, device_id=torch.device("cuda", _device()), timeout=timeout)
-        else:
-            dist.init_process_group(backend, timeout=timeout)
+        # the backends' own connection messages (gloo prints its peer mesh on
+        # stdout) go to stderr: stdout carries only rank 0's JSON line
+        sys.stdout.flush()
+        saved_stdout = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            if backend == "nccl":
+                dist.init_process_group(backend, device_id=torch.device("cuda", _device()), timeout=timeout)
+            else:
+                dist.init_process_group(backend, timeout=timeout)
+        finally:
+            os.dup2(saved_stdout, 1)
+            os.close(saved_stdout)
         coll_dev = "cuda" if backend == "nccl" else "cpu"
         if os.environ.get("GHOSTM_BENCH_NO_BIND") != "1":
             placement = launch.bind_numa(dist, rank, _device())

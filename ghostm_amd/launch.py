@@ -60,7 +60,8 @@ def spawn(argv: list[str], n: int, grace_s: float = 60.0, extra_env: dict | None
         env.update(extra_env or {})
         env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
                     "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), LAUNCH_ENV: "1"})
-        procs.append(subprocess.Popen([sys.executable] + argv, env=env))
+        # only rank 0 reports on stdout; the other ranks' output goes to stderr
+        procs.append(subprocess.Popen([sys.executable] + argv, env=env, stdout=None if r == 0 else sys.stderr))
     status = 0
     failed_at = None
     try:
