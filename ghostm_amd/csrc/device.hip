@@ -197,11 +197,15 @@ static constexpr uint32_t kSlotCap = 256;
 #ifndef GHOSTM_K1_ALIAS
 #define GHOSTM_K1_ALIAS 1
 #endif
+#ifndef GHOSTM_K1_STAGE2  // A/B: a second, hashed bitmap over the queue (kernels.h STAGE2)
+#define GHOSTM_K1_STAGE2 0
+#endif
 constexpr bool kFilterAlias = GHOSTM_K1_ALIAS != 0;
+constexpr bool kFilterStage2 = kFilterAlias && GHOSTM_K1_STAGE2 != 0;
 constexpr uint32_t kFilterScale = kFilterAlias ? 2 : 1;
-#define GHOSTM_FILTER0 kern::k_seed_filter<256, 32768 * kFilterScale, 2304, 1536, kFilterAlias>
-#define GHOSTM_FILTER1 kern::k_seed_filter<512, 65536 * kFilterScale, 4608, 3072, kFilterAlias>
-#define GHOSTM_FILTER2 kern::k_seed_filter<1024, 131072 * kFilterScale, 9216, 6144, kFilterAlias>
+#define GHOSTM_FILTER0 kern::k_seed_filter<256, 32768 * kFilterScale, 2304, 1536, kFilterAlias, kFilterStage2>
+#define GHOSTM_FILTER1 kern::k_seed_filter<512, 65536 * kFilterScale, 4608, 3072, kFilterAlias, kFilterStage2>
+#define GHOSTM_FILTER2 kern::k_seed_filter<1024, 131072 * kFilterScale, 9216, 6144, kFilterAlias, kFilterStage2>
 constexpr size_t FilterLds(size_t cells, size_t table, size_t queue) {
   return ((kFilterAlias ? std::max(cells / 16, table) : cells / 16 + table) + queue) * 4;
 }

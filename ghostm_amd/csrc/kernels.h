@@ -628,11 +628,31 @@ __global__ __launch_bounds__(BLOCK) void k_seed_hash(SeedArgs a) {
 // dead once pass 2 has compacted the queue, the table unused before pass 3),
 // so a larger bitmap (fewer aliased cells, fewer entries queued) fits the same
 // LDS; the table is zeroed after pass 2 instead of with the bitmap.
-template <uint32_t BLOCK, uint32_t FSLOTS, uint32_t TSLOTS, uint32_t QCAP, bool ALIAS = false>
+// STAGE2 (with ALIAS): the queue is filtered once more before the exact
+// table, through a second bitmap in the region's words past the table, with
+// cells by a multiplicative hash of the bin (independent of the first
+// bitmap's low bits). Built from the queued entries only: every entry an
+// emitted bin needs has a partner (the same bin, x - 1 or x + 1) that is itself
+// needed and queued, so the second test drops only lone entries the first
+// bitmap's aliasing let through.
+__host__ __device__ constexpr uint32_t FloorPow2(uint32_t v) {
+  uint32_t p = 1;
+  while (p * 2 <= v) p *= 2;
+  return v ? p : 0;
+}
+__host__ __device__ constexpr uint32_t Log2(uint32_t v) {
+  uint32_t l = 0;
+  while ((1u << (l + 1)) <= v) ++l;
+  return l;
+}
+template <uint32_t BLOCK, uint32_t FSLOTS, uint32_t TSLOTS, uint32_t QCAP, bool ALIAS = false, bool STAGE2 = false>
 __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
   constexpr uint32_t kFWords = FSLOTS / 16;   // 16 two-bit cells per word
   constexpr uint32_t kRegion = ALIAS ? (kFWords > TSLOTS ? kFWords : TSLOTS) : kFWords + TSLOTS;
+  constexpr uint32_t kF2Words = STAGE2 ? FloorPow2(kRegion - TSLOTS) : 0;  // second bitmap (words)
+  static_assert(!STAGE2 || (ALIAS && kF2Words >= 64), "the second bitmap lives past the aliased table");
+  constexpr uint32_t kF2Bits = STAGE2 ? Log2(kF2Words * 16) : 1;
   uint32_t *const s_flt = s_dyn;
   uint32_t *const s_tab = ALIAS ? s_dyn : s_dyn + kFWords;
   uint32_t *const s_q = s_dyn + kRegion;
@@ -870,14 +890,57 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
     qbase += (uint32_t)__popcll(m);
   }
   __syncthreads();
-  const uint32_t qn = s_qn;
+  uint32_t qn = s_qn;
   if (qn > QCAP) {  // block-uniform: redone by k_seed_hash
     if (tid == 0) a.counts[q] = kOverflow;
     return;
   }
-  if constexpr (ALIAS) {  // the bitmap is dead: the exact table takes its place
-    for (uint32_t k = tid; k < TSLOTS / 4; k += BLOCK) reinterpret_cast<uint4 *>(s_tab)[k] = make_uint4(0u, 0u, 0u, 0u);
+  constexpr uint32_t kQPer = (QCAP + BLOCK - 1) / BLOCK;
+  if constexpr (ALIAS) {  // the bitmap is dead: the exact table (and the second bitmap) take its place
+    for (uint32_t k = tid; k < (TSLOTS + kF2Words) / 4; k += BLOCK)
+      reinterpret_cast<uint4 *>(s_tab)[k] = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
+    if constexpr (STAGE2) {
+      uint32_t *const s_f2 = s_tab + TSLOTS;
+      auto cell2 = [](uint32_t x) { return (x * 2654435761u) >> (32 - kF2Bits); };
+      uint32_t xs[kQPer];
+#pragma unroll
+      for (uint32_t u = 0; u < kQPer; ++u) {
+        const uint32_t k = tid + u * BLOCK;
+        xs[u] = k < qn ? s_q[k] : kNone;
+        if (xs[u] != kNone) {
+          const uint32_t c = cell2(xs[u]), sh = (c & 15) * 2;
+          const uint32_t old = atomicOr(&s_f2[c >> 4], 1u << sh);
+          if ((old >> sh) & 1u) atomicOr(&s_f2[c >> 4], 2u << sh);
+        }
+      }
+      if (tid == 0) s_qn = 0;  // every thread read it above; the barrier orders the recount after
+      __syncthreads();
+      auto st = [&](uint32_t x) {
+        const uint32_t c = cell2(x);
+        return (s_f2[c >> 4] >> ((c & 15) * 2)) & 3u;
+      };
+      uint32_t wave_n = 0;
+      unsigned long long bal2[kQPer];
+#pragma unroll
+      for (uint32_t u = 0; u < kQPer; ++u) {
+        const uint32_t x = xs[u];
+        const bool keep = x != kNone && (x <= 1 || (st(x) & 2u) || (st(x - 1) & 1u) || (st(x + 1) & 1u));
+        bal2[u] = __ballot(keep);
+        wave_n += (uint32_t)__popcll(bal2[u]);
+      }
+      uint32_t qb = 0;
+      if (lane == 0 && wave_n) qb = atomicAdd(&s_qn, wave_n);
+      qb = (uint32_t)__shfl((int)qb, 0);
+#pragma unroll
+      for (uint32_t u = 0; u < kQPer; ++u) {
+        const unsigned long long m = bal2[u];
+        if ((m >> lane) & 1ull) s_q[qb + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = xs[u];
+        qb += (uint32_t)__popcll(m);
+      }
+      __syncthreads();
+      qn = s_qn;
+    }
   }
   GHOSTM_K1_PHASE_END(3);
 
@@ -885,7 +948,6 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   //    bin's slot remembers it, so step 4 visits each occupied slot once with
   //    the queue's density (<= QCAP / BLOCK per lane) instead of walking the
   //    table's TSLOTS / BLOCK slots per lane
-  constexpr uint32_t kQPer = (QCAP + BLOCK - 1) / BLOCK;
   BinTable<TSLOTS> table{s_tab};
   uint32_t made[kQPer];
 #pragma unroll
