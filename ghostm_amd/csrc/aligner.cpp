@@ -869,7 +869,13 @@ void Session::DevicePass(QueryData &q, DbData &d, const std::vector<uint32_t> &c
   // segments of ~16M candidates (fewer host round trips per step);
   // GHOSTM_SEGMENT_CANDS / GHOSTM_TAIL_CANDS shrink them so that small test
   // datasets run the many-segment pipeline of the full-size workloads
-  uint64_t kSegmentCands = 16ull << 20, kTailCands = 1ull << 20;
+  // The tail floor is 1 M candidates, or a quarter of a smaller batch, so a
+  // batch of under ~2 M candidates is still cut into three segments whose
+  // formatting overlaps the next one's K2 (cfg2's 0.9 M: 10.2 -> 8.7 ms per
+  // step; at cfg3 and the 125 K shard a smaller floor only adds launches,
+  // profiles/r4_tail_sweep.txt)
+  uint64_t kSegmentCands = 16ull << 20;
+  uint64_t kTailCands = std::min<uint64_t>(1ull << 20, std::max<uint64_t>(1ull << 17, (c_hi - c_lo) / 4));
   if (const char *e = getenv("GHOSTM_SEGMENT_CANDS")) kSegmentCands = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
   if (const char *e = getenv("GHOSTM_TAIL_CANDS")) kTailCands = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
   const uint32_t ng = (uint32_t)q.group_first.size();
