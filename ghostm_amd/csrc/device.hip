@@ -207,7 +207,8 @@ constexpr uint32_t kFilterScale = kFilterAlias ? 2 : 1;
 #define GHOSTM_FILTER1 kern::k_seed_filter<512, 65536 * kFilterScale, 4608, 3072, kFilterAlias, kFilterStage2>
 #define GHOSTM_FILTER2 kern::k_seed_filter<1024, 131072 * kFilterScale, 9216, 6144, kFilterAlias, kFilterStage2>
 constexpr size_t FilterLds(size_t cells, size_t table, size_t queue) {
-  return ((kFilterAlias ? std::max(cells / 16, table) : cells / 16 + table) + queue) * 4;
+  const size_t words = kern::FilterWords((uint32_t)cells);
+  return ((kFilterAlias ? std::max(words, table) : words + table) + queue) * 4;
 }
 constexpr size_t kFilterLds0 = FilterLds(32768 * kFilterScale, 2304, 1536);
 constexpr size_t kFilterLds1 = FilterLds(65536 * kFilterScale, 4608, 3072);

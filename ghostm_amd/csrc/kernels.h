@@ -594,6 +594,12 @@ __global__ __launch_bounds__(BLOCK) void k_seed_hash(SeedArgs a) {
 #ifndef GHOSTM_K1_PREFETCH
 #define GHOSTM_K1_PREFETCH 0
 #endif
+#ifndef GHOSTM_K1_READ2  // filter test reads the word pair (w, w + 1) with one ds_read2_b32 (A/B: 0)
+#define GHOSTM_K1_READ2 0
+#endif
+// the filter bitmap's words: FSLOTS / 16, plus (READ2) a guard word mirroring
+// cells 0 and 1 after the last one, padded to 16 bytes
+__host__ __device__ constexpr uint32_t FilterWords(uint32_t fslots) { return fslots / 16 + (GHOSTM_K1_READ2 ? 4u : 0u); }
 #ifndef GHOSTM_K1_GUARD  // A/B: 1 skips the wave's chunk slots past n by scalar branches
 #define GHOSTM_K1_GUARD 0    // (measured slower: 13.42 against 13.14 ms per class-1 launch)
 #endif
@@ -649,12 +655,13 @@ template <uint32_t BLOCK, uint32_t FSLOTS, uint32_t TSLOTS, uint32_t QCAP, bool 
 __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
   constexpr uint32_t kFWords = FSLOTS / 16;   // 16 two-bit cells per word
-  constexpr uint32_t kRegion = ALIAS ? (kFWords > TSLOTS ? kFWords : TSLOTS) : kFWords + TSLOTS;
+  constexpr uint32_t kFWordsPad = FilterWords(FSLOTS);  // + the READ2 guard word
+  constexpr uint32_t kRegion = ALIAS ? (kFWordsPad > TSLOTS ? kFWordsPad : TSLOTS) : kFWordsPad + TSLOTS;
   constexpr uint32_t kF2Words = STAGE2 ? FloorPow2(kRegion - TSLOTS) : 0;  // second bitmap (words)
   static_assert(!STAGE2 || (ALIAS && kF2Words >= 64), "the second bitmap lives past the aliased table");
   constexpr uint32_t kF2Bits = STAGE2 ? Log2(kF2Words * 16) : 1;
   uint32_t *const s_flt = s_dyn;
-  uint32_t *const s_tab = ALIAS ? s_dyn : s_dyn + kFWords;
+  uint32_t *const s_tab = ALIAS ? s_dyn : s_dyn + kFWordsPad;
   uint32_t *const s_q = s_dyn + kRegion;
   constexpr uint32_t kW = BLOCK / 64;
   constexpr uint32_t KE = 16;                 // entries per lane: n <= 64 * KE * kW
@@ -674,8 +681,8 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   const uint32_t nl = a.nlists;
   // filter bitmap and exact table zeroed with 16-byte stores (both are
   // multiples of four words, s_dyn 16-byte aligned)
-  static_assert(kFWords % 4 == 0 && TSLOTS % 4 == 0, "16-byte zeroing");
-  for (uint32_t k = tid; k < (ALIAS ? kFWords : kFWords + TSLOTS) / 4; k += BLOCK)
+  static_assert(kFWordsPad % 4 == 0 && TSLOTS % 4 == 0, "16-byte zeroing");
+  for (uint32_t k = tid; k < (ALIAS ? kFWordsPad : kFWordsPad + TSLOTS) / 4; k += BLOCK)
     reinterpret_cast<uint4 *>(s_dyn)[k] = make_uint4(0u, 0u, 0u, 0u);
   if (tid == 0) s_qn = 0;
   uint32_t len = 0, beg = 0;
@@ -794,8 +801,11 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
 #pragma unroll
     for (uint32_t u = 0; u < 4; ++u) old[u] = fb[u] ? atomicOr(&s_flt[fw[u]], fb[u]) : 0u;
 #pragma unroll
-    for (uint32_t u = 0; u < 4; ++u)
+    for (uint32_t u = 0; u < 4; ++u) {
       if (old[u] & fb[u]) atomicOr(&s_flt[fw[u]], fb[u] << 1);
+      if (GHOSTM_K1_READ2 && fb[u] && fw[u] == 0 && fb[u] < 16u)  // cells 0 and 1: the guard copy
+        atomicOr(&s_flt[kFWords], (old[u] & fb[u]) ? fb[u] * 3u : fb[u]);
+    }
   }
 #else
   uint32_t bin[KE];
@@ -848,7 +858,9 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
           x = b;
           const uint32_t cell = b & (FSLOTS - 1), sh = (cell & 15) * 2;
           const uint32_t old = atomicOr(&s_flt[cell >> 4], 1u << sh);
-          if ((old >> sh) & 1u) atomicOr(&s_flt[cell >> 4], 2u << sh);
+          const bool twice = (old >> sh) & 1u;
+          if (twice) atomicOr(&s_flt[cell >> 4], 2u << sh);
+          if (GHOSTM_K1_READ2 && cell < 2) atomicOr(&s_flt[kFWords], (twice ? 3u : 1u) << sh);  // guard copy
         }
       }
       bin[e0 + u] = x;
@@ -862,8 +874,16 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   //    cells x - 1, x, x + 1 in bits 0-5 from the words holding x - 1 and
   //    x + 1 (the same word unless the three straddle a word boundary)
   auto near = [&](uint32_t x) {
-    const uint32_t c0 = (x - 1) & (FSLOTS - 1), c2 = (x + 1) & (FSLOTS - 1);
-    return __builtin_amdgcn_alignbit(s_flt[c2 >> 4], s_flt[c0 >> 4], (c0 & 15) * 2);
+    const uint32_t c0 = (x - 1) & (FSLOTS - 1);
+    if constexpr (GHOSTM_K1_READ2) {
+      // words w and w + 1 in one ds_read2_b32: cell x + 1 is in one of them,
+      // and past the last word the guard copy holds cells 0 and 1
+      const uint32_t *w = s_flt + (c0 >> 4);
+      return __builtin_amdgcn_alignbit(w[1], w[0], (c0 & 15) * 2);
+    } else {
+      const uint32_t c2 = (x + 1) & (FSLOTS - 1);
+      return __builtin_amdgcn_alignbit(s_flt[c2 >> 4], s_flt[c0 >> 4], (c0 & 15) * 2);
+    }
   };
   uint32_t wave_n = 0;
   unsigned long long bal[KE];  // wave-uniform: SGPR pairs
