@@ -5,6 +5,10 @@ O=$R/gpurun_out/r4ap
 mkdir -p $O
 cd $R && timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { echo "tests failed"; tail -30 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
+for p in cfg4 cfg2; do
+  GHOSTM_LIB_PATH=$R/ghostm_amd/lib/libghostm_hip_r2on.so timeout -k 10 300 python3 bench.py --preset $p --steps 3 --warmup 1 --no-cpu --no-e2e --workdir /tmp/ap_$p > $O/r2on_$p.json 2> $O/r2on_$p.log || { echo "r2on bench $p failed"; tail -5 $O/r2on_$p.log; exit 1; }
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('r2on bench', sys.argv[2], round(d['ms_per_step'],1), 'ms, matches', d['full_output_matches_reference'], 'k1', round(d['roofline_k1']['ms_per_step'],2))" $O/r2on_$p.json $p
+done
 cd /tmp
 for v in r2on cur r2on cur; do
   L=$R/ghostm_amd/lib/libghostm_hip_$v.so; [ $v = cur ] && L=$R/ghostm_amd/lib/libghostm_hip.so
