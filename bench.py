@@ -223,17 +223,6 @@ def full_pin(preset: str, nq: int, aln: list) -> dict | None:
     return pin
 
 
-def max_hits_per_query(aln: list) -> int:
-    """-b (hits kept per query, reference default 10), as getopt reads it."""
-    best = 10
-    for i, a in enumerate(aln):
-        if a == "-b" and i + 1 < len(aln):
-            best = int(aln[i + 1])
-        elif a.startswith("-b") and len(a) > 2:
-            best = int(a[2:])
-    return best
-
-
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
@@ -264,6 +253,7 @@ def main() -> None:
 
     rank = int(os.environ.get("RANK", "0"))
     dist = None
+    coll_dev = None
     placement = None
     # GHOSTM_BENCH_DIST=1 takes the collective path at world 1 too (under
     # torchrun --nproc-per-node 1): RCCL init, the record gather, the reductions
@@ -344,22 +334,32 @@ def main() -> None:
 
         from ghostm_amd.shard import RecordGather
 
-        # fixed capacity: the most hits any shard can return (queries x -b)
-        b, e = sess.shard_range() if world > 1 else (0, nq)
-        cap = torch.tensor([(min(e, nq) - b) * max_hits_per_query(aln_args)], device=coll_dev, dtype=torch.int64)
+        # fixed capacity: the most records any shard's run can return, as the
+        # library bounds it (its name groups x max(-b, 1), GhostmSessionHitCapacity)
+        cap = torch.tensor([sess.hit_capacity()], device=coll_dev, dtype=torch.int64)
         dist.all_reduce(cap, op=dist.ReduceOp.MAX)
         gatherer = RecordGather(dist, int(cap.item()), HIT_DTYPE.itemsize, coll_dev)
+    fills = {"device_hits_into": 0, "device_hits_copy": 0}  # which fill branch the steps took
+
+    def fill():
+        """The gather payload from the last run's device records."""
+        if coll_dev == "cuda":  # RCCL: the library copies straight into the gather buffer
+            n = sess.device_hits_into(gatherer.payload(), gatherer.cap)
+            fills["device_hits_into"] += 1
+        else:  # gloo rehearsal: the records still leave the GPU by a device copy
+            recs = sess.device_hits()
+            n = recs.numel() // HIT_DTYPE.itemsize
+            if n > gatherer.cap:
+                raise ValueError(f"{n} hit records exceed the gather capacity {gatherer.cap}")
+            gatherer.payload()[: recs.numel()].copy_(recs)
+            fills["device_hits_copy"] += 1
+        gatherer.set_count(n)
 
     def step():
         guarded(sess.run, "run")
         if gatherer is not None:
-            if coll_dev == "cuda":
-                n = sess.device_hits_into(gatherer.payload(), gatherer.cap)
-            else:  # gloo rehearsal: the records still leave the GPU by a device copy
-                recs = sess.device_hits()
-                n = recs.numel() // HIT_DTYPE.itemsize
-                gatherer.payload()[: recs.numel()].copy_(recs)
-            gatherer.set_count(n)
+            # a failing fill (capacity, copy) stops every rank here, not in the gather
+            guarded(fill, "gather fill")
             # the single data-path collective: hit records to rank 0
             gatherer.gather()
 
@@ -383,8 +383,11 @@ def main() -> None:
     sync()
     t = time.perf_counter()
     st_acc = None
+    step_ms = []  # per-step host wall time of this rank (the first shows any one-time stall)
     for _ in range(args.steps):
+        ts = time.perf_counter()
         step()
+        step_ms.append((time.perf_counter() - ts) * 1e3)
         st = sess.stats()
         if st_acc is None:
             st_acc = {k: 0 for k in st}
@@ -422,11 +425,11 @@ def main() -> None:
     matches = None
     gather_check = None
     timed_sha = None  # rank 0: sha256 of the timed run's whole output
-    if world == 1:
+    if dist is None:
         timed_sha = hashlib.sha256(text).hexdigest()
         if pin:
             matches = len(text) == pin["bytes"] and timed_sha == pin["sha256"]
-    else:
+    else:  # also at world 1 under GHOSTM_BENCH_DIST=1: the gather path checks itself
         write_assembled(dist, coll_dev, rank, world, out_path, text)
         # rank 0 checks the last step's gather (the one collective) and the
         # assembled file against an unsharded run of the same queries on its
@@ -447,6 +450,7 @@ def main() -> None:
                 "records_equal_summed_hits": len(gathered) // HIT_DTYPE.itemsize == int(hits.item()),
                 "gathered_records_equal_unsharded": gathered == want_rec,
                 "assembled_file_equals_unsharded": file_sha == hashlib.sha256(want_text).hexdigest(),
+                "records_nonempty": len(gathered) > 0,
             }
             ok_gather = all(v for k, v in gather_check.items() if k != "records_gathered")
             if pin:
@@ -470,11 +474,11 @@ def main() -> None:
             # would free its page-cache pages inside the timed region)
             if rank == 0 and os.path.exists(out_path):
                 os.remove(out_path)
-            # every run starts from a clean page cache, as the first one does: the
-            # previous run's dirty output pages are written back here and the
-            # system given a second to settle, untimed (otherwise the writeback
-            # of the last run's file slowed the next one's writes and reads:
-            # cfg3 runs took 37, 44 and 53 ms in a row, profiles/r4l_e2e/)
+            # every run starts with the previous run's dirty output pages written
+            # back and a second to settle, untimed (otherwise that writeback slowed
+            # the next run's writes and reads: cfg3 runs took 37, 44 and 53 ms in
+            # a row, profiles/r4l_e2e/). The inputs stay in the page cache: the
+            # file loads are warm-cache reads, as for any repeated search of a DB
             os.sync()
             time.sleep(float(os.environ.get("GHOSTM_BENCH_SETTLE_S", "1.0")))
             if dist is not None:
@@ -505,7 +509,8 @@ def main() -> None:
         dt, e2e_res = sorted(runs)[len(runs) // 2]
         e2e = {"seconds": dt, "value": e2e_res / dt, "unit": "query residues/s", "runs_s": [r[0] for r in runs],
                "statistic": f"median of {len(runs)}",
-               "includes": "session create (query/DB/index file loads, H2D; N > 1: rank-local reads and the "
+               "includes": "session create (query/DB/index file loads from a warm page cache, dirty pages written "
+                           "back first; H2D; N > 1: rank-local reads and the "
                            "batch-plan all-gather), the search, text formatting and the output file write "
                            "(N = 1: written while the search runs; N > 1: every rank writes its slice of the "
                            "one file)"}
@@ -601,19 +606,43 @@ def main() -> None:
                     "frac_vop2_alone": ceil_alone / cyc,
                     "effective_clock_ghz": pmc.get("k_score_effective_clock_ghz"),
                 }
+        # K3 per SURVEY §8 d3: TB work = sum over hits of L x the reference's reverse
+        # window (L + 2e*2R columns back from the hit's end, clipped at position 0
+        # and broken at END; aligner.cpp:775, 806-809, 829-830) at 20 ops per cell.
+        # That is exactly the cells k_tb_scan computes (traceback_scan_cells), so
+        # the headline is those cells x 20 over the whole K3 time, against the
+        # packed 16-bit peak the kernels issue at (both K3 kernels are packed
+        # two hits per lane or cheaper). The two kernels are also priced alone:
+        # the scan at K2's 10 ops per cell, the key DP's own cells (columns
+        # 0..j*, strips 0..i*) at 20 ops against the int32 peak (one hit per lane).
         tb_t = per["seconds_traceback"]
-        tb_ach = per["traceback_cells"] * TB_OPS_PER_CELL / tb_t / 1e12 if tb_t > 0 else 0.0
+        tb_scan_t = per.get("seconds_traceback_scan", 0.0)
+        tb_key_t = max(0.0, tb_t - tb_scan_t)
+        scan_cells = per["traceback_scan_cells"]
+        key_cells = per["traceback_cells"]
+        tb_ach = scan_cells * TB_OPS_PER_CELL / tb_t / 1e12 if tb_t > 0 else 0.0
+        scan_ach = scan_cells * SCORE_OPS_PER_CELL / tb_scan_t / 1e12 if tb_scan_t > 0 else 0.0
+        key_ach = key_cells * TB_OPS_PER_CELL / tb_key_t / 1e12 if tb_key_t > 0 else 0.0
         roof_k3 = {
             "bound": "valu",
-            "kernel": "K3 traceback per step (k_tb_scan scores-only reverse scan + k_traceback_key)",
+            "kernel": "K3 traceback per step (k_tb_prep/k_tb_pairs/sorts + k_tb_scan scores-only reverse scan "
+                      "+ k_traceback_key over columns 0..j*)",
+            "definition": "SURVEY §8 d3: sum over hits of L x reverse-window columns (to END / position 0) "
+                          "x 20 ops, / K3 device time per step, vs the packed 16-bit VALU peak",
             "achieved": tb_ach,
-            "peak": PEAK_VALU_TOPS,
+            "peak": PEAK_VALU_PK16_TOPS,
             "unit": "Tops/s",
-            "frac": tb_ach / PEAK_VALU_TOPS,
-            "traceback_cells_per_step": per["traceback_cells"],
-            "scan_cells_per_step": per["traceback_scan_cells"],
+            "frac": tb_ach / PEAK_VALU_PK16_TOPS,
+            "cells_per_step": scan_cells,
             "ops_per_cell": TB_OPS_PER_CELL,
             "ms_per_step": tb_t * 1e3,
+            "scan": {"kernel": "k_tb_scan (+ prep, pairs, the two counting sorts)", "cells_per_step": scan_cells,
+                     "ops_per_cell": SCORE_OPS_PER_CELL, "ms_per_step": tb_scan_t * 1e3,
+                     "tcups": scan_cells / tb_scan_t / 1e12 if tb_scan_t > 0 else 0.0,
+                     "achieved": scan_ach, "peak": PEAK_VALU_PK16_TOPS, "frac": scan_ach / PEAK_VALU_PK16_TOPS},
+            "key_dp": {"kernel": "k_traceback_key (columns 0..j*, strips 0..i*)", "cells_per_step": key_cells,
+                       "ops_per_cell": TB_OPS_PER_CELL, "ms_per_step": tb_key_t * 1e3,
+                       "achieved": key_ach, "peak": PEAK_VALU_TOPS, "frac": key_ach / PEAK_VALU_TOPS},
         }
         seed_gbs = per["seed_bytes"] / per["seconds_seed"] / 1e9 if per["seconds_seed"] > 0 else 0.0
         roof_k1 = {
@@ -645,6 +674,12 @@ def main() -> None:
             "steps": k,
             "warmup": args.warmup,
             "ms_per_step": elapsed / k * 1e3,
+            "step_ms_rank0": step_ms,
+            # value: the resident step (inputs in HBM, the bench contract); SURVEY
+            # §8 d1's wall time of `aln` (file loads, H2D, search, output write) is
+            # value_end_to_end (median of 5 sessions, end_to_end below)
+            "value_is": "resident step: inputs in HBM, search + E-value text per step",
+            "value_end_to_end": e2e["value"] if (e2e and ok) else None,
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -665,6 +700,8 @@ def main() -> None:
             "full_output_matches_reference": matches if pin else None,
             "output_matches_unsharded_run": gather_check["assembled_file_equals_unsharded"] if gather_check else None,
             "gather_check": gather_check,
+            "gather_fill": dict(fills, backend="nccl" if coll_dev == "cuda" else "gloo")
+            if gatherer is not None else None,
             "per_rank": per_rank,
             "full_output_reference": (f"sha256 {pin['sha256'][:16]}..., {pin['lines']} lines "
                                       f"(tests/golden/full_golden.json)") if pin else None,

@@ -98,6 +98,11 @@ class Session:
         native.load().GhostmSessionShardRange(self._h, ctypes.byref(b), ctypes.byref(e))
         return b.value, e.value
 
+    def hit_capacity(self) -> int:
+        """The most hit records one run can return (name groups x max(-b, 1),
+        GhostmSessionHitCapacity): the size of a fixed gather buffer."""
+        return int(native.load().GhostmSessionHitCapacity(self._h))
+
     def run(self, to_file: bool = False) -> None:
         """The search; to_file also writes the -o file while it runs
         (GhostmSessionRunToFile), after which write() is a no-op."""

@@ -1409,9 +1409,7 @@ void Session::Run(bool stream_to_file) {
   hits_.clear();
   hits_valid_ = false;
   Format();  // built here, before any formatting task can need it
-  uint64_t expect = 0;  // the most records the run can append: each group keeps -b hits
-  for (const QueryData &q : queries_) expect += (uint64_t)q.group_first.size() * std::max<uint32_t>(opt_.best, 1);
-  dev.ResetRecords(expect);
+  dev.ResetRecords(HitCapacity());  // the most records the run can append
   records_on_device_ = true;
   const double t0 = NowSeconds();
   TraceMark("run");
@@ -1435,6 +1433,7 @@ void Session::Run(bool stream_to_file) {
   stats_.seconds_seed = dt.seed;
   stats_.seconds_score = dt.score;
   stats_.seconds_traceback = dt.traceback;
+  stats_.seconds_traceback_scan = dt.traceback_scan;
   stats_.score_launches = dt.score_launches;
   stats_.score_launches_packed = dt.score_launches_packed;
   stats_.score_launches_half = dt.score_launches_half;
@@ -1486,6 +1485,12 @@ const std::vector<GhostmHit> &Session::Hits() {
     hits_valid_ = true;
   }
   return hits_;
+}
+
+uint64_t Session::HitCapacity() const {
+  uint64_t n = 0;  // each name group keeps at most -b hits
+  for (const QueryData &q : queries_) n += (uint64_t)q.group_first.size() * std::max<uint32_t>(opt_.best, 1);
+  return n;
 }
 
 size_t Session::DeviceHits(void *dst, size_t cap) {

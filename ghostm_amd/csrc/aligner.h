@@ -128,6 +128,8 @@ class Session {
                    const ShardExchange *exchange = nullptr);
   uint64_t ShardBegin() const { return shard_begin_; }
   uint64_t ShardEnd() const { return shard_end_; }
+  // the most hit records one run can return: name groups x max(-b, 1)
+  uint64_t HitCapacity() const;
   ~Session();
 
   // whole search; replaces previous results. stream_to_file: also write the

@@ -54,6 +54,11 @@ int GhostmSessionShardRange(void *s, uint64_t *begin, uint64_t *end) {
   return 0;
 }
 
+uint64_t GhostmSessionHitCapacity(void *s) {
+  if (!s) return UINT64_MAX;
+  return static_cast<Session *>(s)->HitCapacity();
+}
+
 int GhostmShardCuts(uint64_t n, const uint32_t weights[], const uint8_t group_start[], int world,
                     uint64_t cuts[]) {
   try {

@@ -67,6 +67,7 @@ struct MergePass {
 
 struct DeviceTimes {
   double seed = 0, score = 0, traceback = 0, merge = 0;  // seconds of device time (HIP events)
+  double traceback_scan = 0;  // ... of which K3's scan phase (prep, pairs, sorts, k_tb_scan)
   uint64_t seed_bytes = 0, seed_list_entries = 0;
   uint64_t score_launches = 0, score_launches_packed = 0, score_launches_half = 0;
   uint64_t score_cells = 0, traceback_cells = 0;

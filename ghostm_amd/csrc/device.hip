@@ -176,6 +176,8 @@ struct DeviceModule::Impl {
   std::vector<unsigned long long> h_wide_goff;      // until the next K1, past their async uploads
   hipEvent_t ev_m0 = nullptr, ev_m1 = nullptr;      // K4
   hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;      // K3
+  hipEvent_t ev_tk = nullptr;                       // K3: the scan phase's end (key DP start)
+  bool tk_recorded = false;                         // ... recorded by the last LaunchTraceback
   hipEvent_t ev_done = nullptr, ev_tasks = nullptr; // end of a segment's selection; next tasks uploaded
   // K1 read-backs (per-query bin and candidate counts) land in page-locked
   // staging: GHOSTM_K1_PINNED=0 keeps the pageable copies (A/B)
@@ -265,7 +267,14 @@ void DeviceModule::Bind(int device) {
   HIP_CHECK(hipStreamCreateWithFlags(&c, hipStreamNonBlocking));
   stream_ = s;
   copy_stream_ = c;
-  for (hipEvent_t *e : {&impl_->ev0, &impl_->ev1, &impl_->ev_m0, &impl_->ev_m1, &impl_->ev_t0, &impl_->ev_t1,
+#ifdef GHOSTM_LDS_POISON
+  {  // the pattern every kernel writes over its LDS before its own code runs
+    uint32_t v = 0xA5A5A5A5u;
+    if (const char *e = getenv("GHOSTM_LDS_POISON_PATTERN")) v = (uint32_t)strtoul(e, nullptr, 0);
+    HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(kern::g_lds_poison), &v, sizeof(v)));
+  }
+#endif
+  for (hipEvent_t *e : {&impl_->ev0, &impl_->ev1, &impl_->ev_m0, &impl_->ev_m1, &impl_->ev_t0, &impl_->ev_t1, &impl_->ev_tk,
                         &impl_->ev_done, &impl_->ev_tasks, &impl_->ev_s0, &impl_->ev_s1, &impl_->ev_nb})
     HIP_CHECK(hipEventCreate(e));
   for (hipEvent_t &e : impl_->stage_ev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1144,6 +1153,7 @@ void DeviceModule::Score(DevQuery *q, DevDb *d, uint64_t cand_begin, uint64_t n,
 void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, const DevDb *d, uint32_t pair_span) {
   const uint32_t rows = q->L;
   Impl &I = *impl_;
+  I.tk_recorded = false;
   const Layout lay = ChooseLayout(rows, a.base);
   a.Lpad = lay.Lpad;
   a.G = lay.G;
@@ -1299,6 +1309,9 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
     a.class_off = strips ? class_off : nullptr;
     times_.traceback_launches_strips += strips ? 1 : 0;
     HIP_CHECK(hipGetLastError());
+    // the scan phase (prep, pairs, sorts, K3a) ends here; the key DP follows
+    HIP_CHECK(hipEventRecord(I.ev_tk, S(stream_)));
+    I.tk_recorded = true;
     a.order = I.tb_order2.as<uint32_t>();
     a.ncols = I.tb_ncols.as<uint32_t>();
     a.best_h = I.tb_best.as<uint32_t>();
@@ -1514,6 +1527,7 @@ void DeviceModule::MergeCollect(std::vector<uint32_t> *counts, HostHits *hits) {
   HIP_CHECK(hipStreamSynchronize(S(copy_stream_)));
   times_.merge += ElapsedMs(I.ev_m0, I.ev_m1) * 1e-3;
   times_.traceback += ElapsedMs(I.ev_t0, I.ev_t1) * 1e-3;
+  if (I.tk_recorded) times_.traceback_scan += ElapsedMs(I.ev_t0, I.ev_tk) * 1e-3;
   times_.traceback_cells += cells[0];
   times_.traceback_scan_cells += cells[1];
   times_.traced_hits += cells[2];
@@ -1640,6 +1654,7 @@ void DeviceModule::TraceBack(DevQuery *q, DevDb *d, uint32_t n, const uint32_t *
                            S(stream_)));
   HIP_CHECK(hipStreamSynchronize(S(stream_)));
   times_.traceback += ElapsedMs(I.ev0, I.ev1) * 1e-3;
+  if (I.tk_recorded) times_.traceback_scan += ElapsedMs(I.ev0, I.ev_tk) * 1e-3;
   times_.traceback_cells += cells;
   times_.traceback_scan_cells += scan_cells;
   for (uint32_t i = 0; i < n; ++i) {
@@ -1652,8 +1667,12 @@ void DeviceModule::TraceBack(DevQuery *q, DevDb *d, uint32_t n, const uint32_t *
 }
 
 const char *DeviceBuildInfo() {
-  return "ghostm_hip gfx950: K1 k_seed<LDS|global merge-path>, K2 k_score<S=8|16|32> "
-         "lane-group int32, K3 k_traceback<S=8|16|32>";
+  return "ghostm_hip gfx950: K1 k_seed_lists/k_seed_filter/k_seed_hash/k_seed, K2 k_score16f/k_score16/k_score, "
+         "K3 k_tb_scan/k_traceback_key/k_traceback, K4 k_merge_wave/k_merge"
+#ifdef GHOSTM_LDS_POISON
+         "; LDS poison build"
+#endif
+      ;
 }
 
 // ============================================================ reference C ABI

@@ -31,6 +31,31 @@
 namespace ghostm {
 namespace kern {
 
+// LDS poison build (-DGHOSTM_LDS_POISON=1, ghostm_amd/lib/libghostm_hip_poison.so):
+// every kernel first fills its whole LDS allocation, static and dynamic (the
+// dispatch packet's group_segment_size), with g_lds_poison, so a read of LDS
+// the kernel never wrote returns that pattern instead of whatever an earlier
+// workgroup left there. Tests run the golden variants under two patterns: a
+// result that depends on such a read differs under one of them.
+#ifdef GHOSTM_LDS_POISON
+__device__ uint32_t g_lds_poison = 0xA5A5A5A5u;  // set at Bind from GHOSTM_LDS_POISON_PATTERN
+__device__ __forceinline__ void PoisonLds() {
+  // hsa_kernel_dispatch_packet_t: group_segment_size at byte 28
+  typedef const __attribute__((address_space(4))) uint32_t *PacketWords;
+  const uint32_t bytes = ((PacketWords)__builtin_amdgcn_dispatch_ptr())[7];
+  const uint32_t v = g_lds_poison;
+  const uint32_t nthreads = blockDim.x * blockDim.y * blockDim.z;
+  const uint32_t tid = threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z);
+  for (uint32_t off = tid * 4; off + 4 <= bytes; off += nthreads * 4)
+    asm volatile("ds_write_b32 %0, %1" : : "v"(off), "v"(v) : "memory");
+  asm volatile("s_waitcnt lgkmcnt(0)" : : : "memory");
+  __syncthreads();
+}
+#define GHOSTM_POISON_LDS() ::ghostm::kern::PoisonLds()
+#else
+#define GHOSTM_POISON_LDS() ((void)0)
+#endif
+
 constexpr uint32_t kSeqEnd = 25;
 constexpr uint32_t kPadCode = 31;      // unused residue code: query padding rows
 constexpr int kNeg = -30000;           // score of a padding row (keeps it at 0)
@@ -65,6 +90,7 @@ struct SeedListArgs {
 };
 
 __global__ __launch_bounds__(256) void k_seed_lists(SeedListArgs a) {
+  GHOSTM_POISON_LDS();
   const uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63;
   if (q >= a.nq) return;
@@ -176,6 +202,7 @@ __device__ inline uint32_t UpperIndex(const uint32_t *off, uint32_t hi, uint32_t
 
 template <uint32_t BLOCK, uint32_t CAP, bool GBUF>
 __global__ __launch_bounds__(BLOCK) void k_seed(SeedArgs a) {
+  GHOSTM_POISON_LDS();
   __shared__ uint32_t s_beg[kMaxLists];
   __shared__ uint32_t s_off[kMaxLists + 1];
   __shared__ uint32_t s_part[BLOCK / 64];
@@ -511,6 +538,7 @@ __device__ __forceinline__ void EmitFromTable(const SeedArgs &a, uint32_t q, uin
 
 template <uint32_t BLOCK, uint32_t TSLOTS>
 __global__ __launch_bounds__(BLOCK) void k_seed_hash(SeedArgs a) {
+  GHOSTM_POISON_LDS();
   extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];  // TSLOTS words (dynamic)
   constexpr uint32_t kChunks = TSLOTS / 64;  // the class caps keep n <= TSLOTS
   __shared__ uint32_t s_beg[kMaxLists];
@@ -653,6 +681,7 @@ __host__ __device__ constexpr uint32_t Log2(uint32_t v) {
 }
 template <uint32_t BLOCK, uint32_t FSLOTS, uint32_t TSLOTS, uint32_t QCAP, bool ALIAS = false, bool STAGE2 = false>
 __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
+  GHOSTM_POISON_LDS();
   extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
   constexpr uint32_t kFWords = FSLOTS / 16;   // 16 two-bit cells per word
   constexpr uint32_t kFWordsPad = FilterWords(FSLOTS);  // + the READ2 guard word
@@ -1014,6 +1043,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
 __global__ void k_compact(const uint32_t *slots, uint32_t slot_cap, const uint32_t *counts,
                           const uint8_t *in_slot, const unsigned long long *offsets,
                           uint32_t nq, uint32_t *out_start, uint32_t *out_qid) {
+  GHOSTM_POISON_LDS();
   const uint32_t q = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   if (q >= nq) return;
   const uint32_t c = counts[q];
@@ -1066,6 +1096,7 @@ struct ScoreArgs {
 
 template <int S>
 __global__ __launch_bounds__(kScoreBlock) void k_score(ScoreArgs a) {
+  GHOSTM_POISON_LDS();
   extern __shared__ __attribute__((aligned(16))) int s_prof[];
   const ScoreTask t = a.tasks[blockIdx.x];
   const uint32_t RS = a.Lpad + 4;  // padded profile row (spreads LDS banks)
@@ -1423,6 +1454,7 @@ __device__ __forceinline__ void BuildProfileUnit(const ScoreArgs &a, const Score
 
 template <int S, bool HALF>
 __global__ __launch_bounds__(kScoreBlock) void k_score16(ScoreArgs a) {
+  GHOSTM_POISON_LDS();
   using C = Cells<HALF>;
   extern __shared__ __attribute__((aligned(16))) short s_prof16[];
   const ScoreTask t = a.tasks[blockIdx.x];
@@ -1643,6 +1675,7 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16(ScoreArgs a) {
 // query to fill its blocks).
 template <int S, bool SWAR = false, bool UNIT = false>
 __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
+  GHOSTM_POISON_LDS();
   static_assert(!UNIT || SWAR, "unit-pair words carry integer patterns");
   using C = Cells<true>;
   extern __shared__ __attribute__((aligned(16))) short s_prof16[];
@@ -2028,6 +2061,7 @@ __device__ inline uint32_t WaveMax(uint32_t v) {
 
 template <int S>
 __global__ __launch_bounds__(kTbBlock) void k_traceback(TbArgs a) {
+  GHOSTM_POISON_LDS();
   __shared__ int s_mat[32 * 32];
   for (uint32_t e = threadIdx.x; e < 32 * 32; e += kTbBlock) s_mat[e] = a.mat_tb[e];
   __syncthreads();
@@ -2167,6 +2201,7 @@ __device__ inline int ShiftUpI(int v) { return __builtin_amdgcn_update_dpp(0, v,
 
 template <int S, int MLW, bool FINAL>
 __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
+  GHOSTM_POISON_LDS();
   using KL = KeyLayout<MLW>;
   // rows of 33 dwords: lanes reading the same query code for different DB codes
   // fall on different banks
@@ -2489,6 +2524,7 @@ __device__ inline void MergeGroup(const MergeArgs &a, uint32_t g) {
 }
 
 __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
+  GHOSTM_POISON_LDS();
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g < a.ng) MergeGroup(a, g);
 }
@@ -2708,6 +2744,7 @@ __device__ inline void MergeWaveGroup(const MergeArgs &a, uint32_t g, uint32_t l
 // waves per CU of the 1024-key rows), then CAP = kMergeCap for the rest.
 template <uint32_t CAP, bool SMALL>
 __global__ __launch_bounds__(64 * kMergeWaves) void k_merge_wave(MergeArgs a) {
+  GHOSTM_POISON_LDS();
   __shared__ unsigned long long s_key[kMergeWaves][CAP];
   __shared__ uint16_t s_ls[kMergeWaves][CAP + 2];
   __shared__ uint16_t s_rs[kMergeWaves][CAP + 2];
@@ -2731,6 +2768,7 @@ __global__ void k_finalize(const uint32_t *sel_count, const uint32_t *sel_score,
                            const uint32_t *subj_start, uint32_t ng, uint32_t cap, uint32_t chunk,
                            const uint32_t *sel_from, const SlotHit *carry, SlotHit *out,
                            unsigned long long *traced) {
+  GHOSTM_POISON_LDS();
   __shared__ uint32_t s_fresh;
   if (threadIdx.x == 0) s_fresh = 0;
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;  // slots = ng * cap < 2^32
@@ -2768,6 +2806,7 @@ struct HitRecord32 {
 __global__ void k_records(const uint32_t *sel_count, const SlotHit *slots, const uint32_t *prefix,
                           const uint32_t *group_last, uint32_t ng, uint32_t cap, uint32_t q_base,
                           const uint32_t *chunk_base, HitRecord32 *out) {
+  GHOSTM_POISON_LDS();
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= ng) return;
   const uint32_t n = sel_count[g], at = prefix[g], qid = q_base + group_last[g];
@@ -2822,6 +2861,7 @@ __global__ __launch_bounds__(256) void k_tb_prep(const uint32_t *qid, const uint
                                                  uint32_t base, const uint32_t *subj, uint32_t nsubj,
                                                  const uint32_t *subj_bucket, uint32_t dblen, uint32_t *width,
                                                  uint32_t *ncols, uint32_t *skey, uint32_t *empty) {
+  GHOSTM_POISON_LDS();
   __shared__ uint32_t s_empty;
   if (threadIdx.x == 0) s_empty = 0;
   __syncthreads();
@@ -2855,6 +2895,7 @@ constexpr uint32_t kPairRun = 32;  // longer runs are paired 32 slots at a time
 __global__ __launch_bounds__(256) void k_tb_pairs(const uint32_t *qid, const uint32_t *width, uint32_t n,
                                                   uint32_t span, uint32_t *pair_a, uint32_t *pair_b,
                                                   uint32_t *key, uint32_t *hist) {
+  GHOSTM_POISON_LDS();
   __shared__ uint32_t s_hist[kSortBins];
   __shared__ uint32_t s_total;
   for (uint32_t b = threadIdx.x; b < kSortBins; b += blockDim.x) s_hist[b] = 0;
@@ -2926,6 +2967,7 @@ constexpr uint32_t kCsortTile = 256 * kCsortItems;
 __global__ __launch_bounds__(256) void k_csort_scatter(const uint32_t *key, uint32_t n, bool skip_zero,
                                                        const uint32_t *hist, uint32_t *cursor,
                                                        uint32_t *order, uint32_t *class_off = nullptr) {
+  GHOSTM_POISON_LDS();
   static_assert(kSortBins == 4 * 256 && kSortBins == 1024, "four bins per thread, ten key bits");
   __shared__ uint32_t s_pre[kSortBins];
   __shared__ uint32_t s_cnt[kSortBins];
@@ -3017,6 +3059,7 @@ struct TbScanArgs {
 // processing order (row U at position Lpad-1-U; padding rows kPadCode), four per
 // word: lane i of a lane group reads its S/4 words as aligned 16-byte loads.
 __global__ void k_rev_codes(const uint8_t *qseq, uint32_t nq, uint32_t L, uint32_t Lpad, uint32_t *out) {
+  GHOSTM_POISON_LDS();
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t words = Lpad / 4;
   if (t >= (size_t)nq * words) return;
@@ -3047,6 +3090,7 @@ __global__ void k_rev_codes(const uint8_t *qseq, uint32_t nq, uint32_t L, uint32
 // the halves, and the packed f16 maxima order the patterns as integers).
 template <int S, bool HALF, bool EXACT, bool FRAMED = false, bool SWAR = false, bool PRIV = false>
 __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
+  GHOSTM_POISON_LDS();
   using C = Cells<HALF>;
   static_assert(!FRAMED || HALF, "the frame is an f16 kernel");
   static_assert(!SWAR || FRAMED, "integer patterns: the framed kernel");

@@ -9,7 +9,7 @@ multi-GPU path needs.
   parent's output. The parent waits; when a child fails it gives the others a
   grace period (they fail on their own through `agree`) and then kills them.
   Its exit status is the first failing child's, else 0.
-* `bind_numa`: pins a rank's threads to the CPUs next to its GPU
+* `bind_numa`: pins every thread of a rank to the CPUs next to its GPU
   (`/sys/bus/pci/devices/<bdf>/local_cpulist`), split disjointly among the
   ranks of this host that share those CPUs, and sets GHOSTM_THREADS to the
   rank's share so the library's formatting pool matches it.
@@ -166,16 +166,37 @@ def bind_numa(dist, rank: int, device: int) -> dict:
     local_world = sum(1 for k in keys if k[0] == info["host"])
     quota = cgroup_cpus()
     threads = max(1, min(16, len(mine), (quota // local_world) if quota else len(mine)))
-    try:
-        os.sched_setaffinity(0, mine)
-        info["bound"] = True
-    except OSError as e:
-        info["bound"] = False
-        info["error"] = str(e)
+    # every thread of the process: sched_setaffinity(0) pins only the calling
+    # thread, and the HIP runtime, RCCL and gloo have started theirs by now
+    bound, failed = bind_threads(mine)
+    info["bound"] = bound > 0 and not failed
+    info["threads_bound"] = bound
+    if failed:
+        info["error"] = f"{len(failed)} thread(s) could not be bound: {failed[0]}"
     os.environ["GHOSTM_THREADS"] = str(threads)
     info.update({"numa_local": local is not None, "cpus": _fmt_cpulist(mine), "threads": threads,
                  "ranks_sharing_cpus": len(sharing)})
     return info
+
+
+def bind_threads(cpus: list[int]) -> tuple[int, list[str]]:
+    """Set the CPU affinity of every thread of this process (each TID under
+    /proc/self/task; threads created later inherit it from their creator).
+    Returns (threads bound, errors)."""
+    try:
+        tids = sorted(int(t) for t in os.listdir("/proc/self/task"))
+    except OSError:
+        tids = [0]
+    bound, failed = 0, []
+    for tid in tids:
+        try:
+            os.sched_setaffinity(tid, cpus)
+            bound += 1
+        except ProcessLookupError:  # the thread ended meanwhile
+            continue
+        except OSError as e:
+            failed.append(f"tid {tid}: {e}")
+    return bound, failed
 
 
 def _fmt_cpulist(cpus: list[int]) -> str:

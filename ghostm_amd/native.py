@@ -79,6 +79,7 @@ class GhostmStats(ctypes.Structure):
         ("seed_list_entries", c_uint64),
         ("score_launches_unit", c_uint64),
         ("traceback_launches_strips", c_uint64),
+        ("seconds_traceback_scan", ctypes.c_double),
     ]
 
     def as_dict(self) -> dict:
@@ -120,6 +121,7 @@ SIGNATURES = {
     "GhostmSessionCreateShard": (c_void_p, [c_int, POINTER(c_char_p), c_int, c_int]),
     "GhostmSessionCreateShardEx": (c_void_p, [c_int, POINTER(c_char_p), c_int, c_int, c_void_p, c_void_p]),
     "GhostmSessionShardRange": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
+    "GhostmSessionHitCapacity": (c_uint64, [c_void_p]),
     "GhostmShardCuts": (c_int, [c_uint64, u32p, POINTER(ctypes.c_uint8), c_int, POINTER(c_uint64)]),
     "GhostmSessionRun": (c_int, [c_void_p]),
     "GhostmSessionRunToFile": (c_int, [c_void_p]),

@@ -204,6 +204,8 @@ typedef struct GhostmStats {
   uint64_t seed_list_entries;       /* K1: sum over queries of the k-mer position-list lengths */
   uint64_t score_launches_unit;     /* framed integer-pattern K2 launches with unit-pair profile words (k_score16f<S, true, true>) */
   uint64_t traceback_launches_strips; /* K3 key DPs run by strip class (each hit on the strips up to its first maximal cell) */
+  double seconds_traceback_scan;    /* of seconds_traceback: the scan phase (k_tb_prep, k_tb_pairs, the sorts,
+                                       k_tb_scan); the rest is the key DP (k_traceback_key) */
 } GhostmStats;
 
 /* Session: parse `aln` options exactly like the reference (getopt string
@@ -255,6 +257,13 @@ void *GhostmSessionCreateShardEx(int argc, char **argv, int rank, int world, Gho
 /* The query range [begin, end) of a shard session, as indices over the
  * selected chunks' queries (0, UINT64_MAX for an unsharded session). */
 int GhostmSessionShardRange(void *session, uint64_t *begin, uint64_t *end);
+
+/* The most hit records one run of this session can return: its name groups x
+ * max(-b, 1) (each group keeps at most -b hits, reference aligner.cpp:742-760;
+ * -b is read with atoi as aligner.cpp:251 does). A caller sizes its
+ * GhostmSessionDeviceHits destination, or a fixed-capacity gather buffer, from
+ * it. Returns UINT64_MAX for a null session. */
+uint64_t GhostmSessionHitCapacity(void *session);
 
 /* The shard rule on its own (host only, no device): cuts[0..world] over n
  * queries of the given weights; a cut falls only where group_start[i] != 0 and

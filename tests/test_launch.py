@@ -108,6 +108,8 @@ PLACE = textwrap.dedent("""
     dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=60))
     info = launch.bind_numa(dist, dist.get_rank(), 0)
     info["affinity"] = sorted(os.sched_getaffinity(0))
+    # every thread, including those gloo started before the binding
+    info["thread_affinity"] = [sorted(os.sched_getaffinity(int(t))) for t in os.listdir("/proc/self/task")]
     info["env_threads"] = os.environ["GHOSTM_THREADS"]
     out = [None] * dist.get_world_size()
     dist.all_gather_object(out, info)
@@ -136,6 +138,8 @@ def test_bind_numa_gives_disjoint_cpu_shares(tmp_path):
     for o in out:
         assert o["ranks_sharing_cpus"] == 2
         assert int(o["env_threads"]) == o["threads"] >= 1
+        assert o["bound"] and o["threads_bound"] > 1  # the backend's threads too
+        assert all(t == o["affinity"] for t in o["thread_affinity"]), o["thread_affinity"]
 
 
 GATHER = textwrap.dedent("""
