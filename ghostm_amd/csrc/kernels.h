@@ -628,6 +628,9 @@ __global__ __launch_bounds__(BLOCK) void k_seed_hash(SeedArgs a) {
 // the filter bitmap's words: FSLOTS / 16, plus (READ2) a guard word mirroring
 // cells 0 and 1 after the last one, padded to 16 bytes
 __host__ __device__ constexpr uint32_t FilterWords(uint32_t fslots) { return fslots / 16 + (GHOSTM_K1_READ2 ? 4u : 0u); }
+#ifndef GHOSTM_K1_BATCH  // A/B: pass 1 with buffer loads and the four entries' marks batched
+#define GHOSTM_K1_BATCH 0   // (branch-free bins, all four ds_or_rtn issued before the first wait)
+#endif
 #ifndef GHOSTM_K1_GUARD  // A/B: 1 skips the wave's chunk slots past n by scalar branches
 #define GHOSTM_K1_GUARD 0    // (measured slower: 13.42 against 13.14 ms per class-1 launch)
 #endif
@@ -859,6 +862,48 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
     // branch below and waits for them one entry at a time)
 #pragma unroll
     for (uint32_t u = 0; u < 4; ++u) asm volatile("" : "+v"(dd[u]));
+#if GHOSTM_K1_BATCH
+    // positions through a raw buffer (32-bit offsets, no 64-bit address math);
+    // entries past n read entry 0's word (any valid one) and are dropped below
+    const __amdgpu_buffer_rsrc_t pr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)a.positions, 0, 0x7FFFFFFF, 0x00020000);
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) {
+      const bool in = ii[u] < n;
+      const uint32_t at = in ? ii[u] + dd[u] : 0u;  // = list_beg[j] + (i - s_off[j])
+      pos[u] = __builtin_amdgcn_raw_buffer_load_b32(pr, at * 4, 0, 0);
+      lst[u] = in ? jj[u] : kNone;
+      prv[u] = kNone;
+      if (lane == 0 && in && ii[u] != s_off[jj[u]]) prv[u] = __builtin_amdgcn_raw_buffer_load_b32(pr, at * 4 - 4, 0, 0);
+    }
+    // bins and the duplicate test without branches, then the four entries'
+    // marks issued together (an entry with no bin ORs 0 into the word of its
+    // lane's index: no same-address atomics among them)
+    uint32_t fw[4], fb[4], old[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) {
+      const uint32_t j = lst[u];
+      const uint32_t pj = ShiftUp(j), pp = ShiftUp(pos[u]);
+      const uint32_t prev_pos = (lane > 0 && pj == j) ? pp : prv[u];
+      const uint32_t d0 = __umul24(j, a.shift);
+      const uint32_t b = (pos[u] - d0) >> a.log_region;
+      const bool dup = prev_pos != kNone && ((prev_pos - d0) >> a.log_region) == b;
+      const bool live = j != kNone && !dup;
+      const uint32_t x = live ? b : kNone;
+      bin[e0 + u] = x;
+      const uint32_t cell = x & (FSLOTS - 1);
+      fw[u] = live ? cell >> 4 : lane;
+      fb[u] = live ? 1u << ((cell & 15) * 2) : 0u;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) old[u] = atomicOr(&s_flt[fw[u]], fb[u]);
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) {
+      if (old[u] & fb[u]) atomicOr(&s_flt[fw[u]], fb[u] << 1);
+      if (GHOSTM_K1_READ2 && fb[u] && fw[u] == 0 && fb[u] < 16u)  // cells 0 and 1: the guard copy
+        atomicOr(&s_flt[kFWords], (old[u] & fb[u]) ? fb[u] * 3u : fb[u]);
+    }
+#else
 #pragma unroll
     for (uint32_t u = 0; u < 4; ++u) {
       const uint32_t i = ii[u], j = jj[u];
@@ -894,6 +939,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
       }
       bin[e0 + u] = x;
     }
+#endif
   }
 #endif
   __syncthreads();
@@ -3055,6 +3101,10 @@ struct TbScanArgs {
   uint32_t strips;
 };
 
+#ifndef GHOSTM_K3_ROWOFF  // A/B: the scan keeps each row's table offset in its own register
+#define GHOSTM_K3_ROWOFF 0   // (a VOP2 address add per row instead of an SDWA byte extract)
+#endif
+
 // Per query, the table byte offsets (code * 4) of its rows in the reverse DP's
 // processing order (row U at position Lpad-1-U; padding rows kPadCode), four per
 // word: lane i of a lane group reads its S/4 words as aligned 16-byte loads.
@@ -3164,6 +3214,16 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
         qoff[1] = v.y;
       }
     }
+    // ROWOFF: each row's byte offset unpacked into a register of its own
+    constexpr bool kRowOff = GHOSTM_K3_ROWOFF && !PRIV;
+    uint32_t roff[kRowOff ? S : 1];
+    if constexpr (kRowOff) {
+#pragma unroll
+      for (int u = 0; u < S; ++u) {
+        roff[u] = (qoff[u >> 2] >> (8 * (u & 3))) & 0xFFu;
+        asm volatile("" : "+v"(roff[u]));  // opaque: not folded back into SDWA extracts
+      }
+    }
     // PRIV: each row's byte offset in the bank-private table (query code part
     // plus this lane's bank); the column adds its DB code's part
     uint32_t rp[PRIV ? S : 1];
@@ -3257,6 +3317,8 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
         if constexpr (PRIV) {
           return make_uint2(*reinterpret_cast<const uint32_t *>(tpa + rp[u]),
                             *reinterpret_cast<const uint32_t *>(tpb + rp[u]));
+        } else if constexpr (kRowOff) {
+          return *reinterpret_cast<const uint32_t *>(tp + roff[u]);
         } else {
           return *reinterpret_cast<const uint32_t *>(tp + ((qoff[u >> 2] >> (8 * (u & 3))) & 0xFFu));
         }
