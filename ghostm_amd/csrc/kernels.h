@@ -628,8 +628,12 @@ __global__ __launch_bounds__(BLOCK) void k_seed_hash(SeedArgs a) {
 // the filter bitmap's words: FSLOTS / 16, plus (READ2) a guard word mirroring
 // cells 0 and 1 after the last one, padded to 16 bytes
 __host__ __device__ constexpr uint32_t FilterWords(uint32_t fslots) { return fslots / 16 + (GHOSTM_K1_READ2 ? 4u : 0u); }
-#ifndef GHOSTM_K1_BATCH  // A/B: pass 1 with buffer loads and the four entries' marks batched
-#define GHOSTM_K1_BATCH 0   // (branch-free bins, all four ds_or_rtn issued before the first wait)
+// Pass 1 with buffer loads and the four entries' marks batched (branch-free
+// bins, all four ds_or_rtn issued before the first wait): K1 28.7 -> 27.85 ms
+// per cfg4 step, same box (profiles/r5b/ab.txt). GHOSTM_K1_BATCH=0 keeps the
+// per-entry branches (A/B).
+#ifndef GHOSTM_K1_BATCH
+#define GHOSTM_K1_BATCH 1
 #endif
 #ifndef GHOSTM_K1_GUARD  // A/B: 1 skips the wave's chunk slots past n by scalar branches
 #define GHOSTM_K1_GUARD 0    // (measured slower: 13.42 against 13.14 ms per class-1 launch)
@@ -3101,8 +3105,12 @@ struct TbScanArgs {
   uint32_t strips;
 };
 
-#ifndef GHOSTM_K3_ROWOFF  // A/B: the scan keeps each row's table offset in its own register
-#define GHOSTM_K3_ROWOFF 0   // (a VOP2 address add per row instead of an SDWA byte extract)
+// The scan keeps each row's table offset in its own register: a VOP2 address
+// add per row instead of an SDWA byte extract (which issues at the VOP3 rate),
+// 162 VGPRs, still 3 waves per SIMD: K3 51.25 -> 50.5 ms per cfg4 step, same
+// box (profiles/r5b/ab.txt). GHOSTM_K3_ROWOFF=0 keeps the packed bytes (A/B).
+#ifndef GHOSTM_K3_ROWOFF
+#define GHOSTM_K3_ROWOFF 1
 #endif
 
 // Per query, the table byte offsets (code * 4) of its rows in the reverse DP's
