@@ -1165,19 +1165,17 @@ constexpr uint32_t kIdLen = 512, kIdMatch = 128;
 // bytes. A hit copies the 16 bytes straight from the two loaded words into the
 // line (which has kFixed bytes of room) and steps on by the length: no reload
 // from a stack buffer at an odd offset, which stalled on store forwarding. The
-// storage comes zeroed from calloc (the OS's zero pages), so a table costs
-// nothing until entries are used: the session's create -> run path no longer
-// formats 60 K identity strings up front.
+// storage comes zeroed from the OS (HostAlloc: huge pages when large), so a
+// table costs nothing until entries are used: the session's create -> run
+// path no longer formats 60 K identity strings up front.
 struct TextCache {
   struct Entry {
     std::atomic<uint64_t> a, b;
   };
   Entry *e = nullptr;
   size_t n = 0;
-  explicit TextCache(size_t entries) : e(static_cast<Entry *>(std::calloc(entries, sizeof(Entry)))), n(entries) {
-    if (!e) throw std::bad_alloc();
-  }
-  ~TextCache() { std::free(e); }
+  explicit TextCache(size_t entries) : e(static_cast<Entry *>(HostAlloc(entries * sizeof(Entry)))), n(entries) {}
+  ~TextCache() { HostFree(e, n * sizeof(Entry)); }
   TextCache(const TextCache &) = delete;
   TextCache &operator=(const TextCache &) = delete;
   // the text of entry k, made by make(buf) (writes at most 15 bytes, returns its end) on first use
@@ -1279,17 +1277,12 @@ struct LineFormat {
 };
 
 namespace {
-// Appends lines through a raw cursor into a std::string that grows in chunks.
+// Appends lines through a raw cursor into a part's text buffer.
 struct TextCursor {
-  std::string &s;
-  size_t used;
-  explicit TextCursor(std::string &str) : s(str), used(str.size()) {}
-  char *Reserve(size_t need) {
-    if (s.size() < used + need) s.resize(std::max(used + need, s.size() * 2 + 4096));
-    return &s[used];
-  }
-  void Commit(char *end) { used = (size_t)(end - s.data()); }
-  ~TextCursor() { s.resize(used); }
+  TextBuf &s;
+  explicit TextCursor(TextBuf &buf) : s(buf) {}
+  char *Reserve(size_t need) { return s.Reserve(need); }
+  void Commit(char *end) { s.Commit(end); }
 };
 }  // namespace
 
@@ -1301,8 +1294,8 @@ const LineFormat &Session::Format() {
 void Session::Part::Reset(size_t pieces) {
   text.resize(pieces);
   hits.resize(pieces);
-  for (std::string &t : text) t.clear();
-  for (std::vector<GhostmHit> &h : hits) h.clear();
+  for (TextBuf &t : text) t.clear();
+  for (HitVec &h : hits) h.clear();
 }
 
 Session::Part *Session::NewPart() {
@@ -1316,7 +1309,7 @@ void Session::FormatResults(const QueryData &q, const Results &results, Part *ou
   const LineFormat &w = Format();
   ParallelFor(n, threads_, [&](size_t b, size_t e, unsigned t) {
     TextCursor text(out->text[t]);
-    std::vector<GhostmHit> &hits = out->hits[t];
+    HitVec &hits = out->hits[t];
     for (size_t i = b; i < e; ++i) {
       const uint64_t space = (uint64_t)q.qlen[i] * (uint64_t)db_sum_u32_;
       const float scaled = (float)space * w.ev.p.K;
@@ -1342,7 +1335,7 @@ void Session::FormatSelected(const QueryData &q, uint32_t g0, const std::vector<
   out->Reset(workers);
   const LineFormat &w = Format();
   ParallelFor(ng, workers, [&](size_t b, size_t e, unsigned t) {
-    std::vector<GhostmHit> &ph = out->hits[t];
+    HitVec &ph = out->hits[t];
     size_t nh = 0;
     for (size_t g = b; g < e; ++g) nh += counts[g];
     out->text[t].reserve(nh * 96);
@@ -1467,11 +1460,11 @@ const std::string &Session::Output() {
   if (!joined_valid_) {
     size_t n = 0;
     for (size_t k = 0; k < used_parts_; ++k)
-      for (const std::string &t : parts_[k].text) n += t.size();
+      for (const TextBuf &t : parts_[k].text) n += t.size();
     joined_.clear();
     joined_.reserve(n);
     for (size_t k = 0; k < used_parts_; ++k)
-      for (const std::string &t : parts_[k].text) joined_.append(t);
+      for (const TextBuf &t : parts_[k].text) joined_.append(t.data(), t.size());
     joined_valid_ = true;
   }
   return joined_;
@@ -1508,7 +1501,7 @@ size_t Session::DeviceHits(void *dst, size_t cap) {
 void Session::PartDone(const Part *part) {
   if (stream_fd_ < 0) return;
   writer_->Submit([this, part] {
-    for (const std::string &t : part->text) {
+    for (const TextBuf &t : part->text) {
       const char *p = t.data();
       size_t left = t.size();
       while (left && !stream_failed_) {
@@ -1536,12 +1529,12 @@ void Session::WriteOutputFile() {
   } done;
   // the pieces in output order, written at their offsets by parallel threads
   // (an unwritable path writes nothing, as the reference's unchecked ofstream)
-  std::vector<const std::string *> pieces;
+  std::vector<const TextBuf *> pieces;
   std::vector<uint64_t> at;
   uint64_t total = 0;
   for (size_t k = 0; k < used_parts_; ++k)
-    for (const std::string &t : parts_[k].text) {
-      if (t.empty()) continue;
+    for (const TextBuf &t : parts_[k].text) {
+      if (!t.size()) continue;
       pieces.push_back(&t);
       at.push_back(total);
       total += t.size();
