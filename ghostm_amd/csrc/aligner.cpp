@@ -1449,6 +1449,7 @@ void Session::Run(bool stream_to_file) {
   stats_.seed_filter_overflows = dt.seed_filter_overflows;
   stats_.score_launches_swar = dt.score_launches_swar;
   stats_.score_launches_unit = dt.score_launches_unit;
+  stats_.score_launches_pair = dt.score_launches_pair;
   stats_.traceback_launches_strips = dt.traceback_launches_strips;
   stats_.traceback_launches_scan_swar = dt.traceback_launches_scan_swar;
   stats_.tracebacks += dt.traced_hits;  // device merge (the host merge counts its own)

@@ -84,6 +84,7 @@ struct DeviceTimes {
   uint64_t traceback_launches_strips = 0;  // key DPs run by strip class (lanes of strips 0..i* only)
   uint64_t score_launches_swar = 0;  // ... of the framed kernel over 16-bit integer patterns (k_score16f<S, true>)
   uint64_t score_launches_unit = 0;  // ... of its unit-pair profile variant (k_score16f<S, true, true>)
+  uint64_t score_launches_pair = 0;  // sparse segments: the pair-table kernel (k_score_pair)
   uint64_t seed_filter_overflows = 0;             // ... queries redone by k_seed_hash (queue overflow)
   uint64_t traced_hits = 0;                       // device merge: hits selected from new candidates (K3 run)
 };

@@ -98,6 +98,8 @@ struct DevQuery {
   DevBuf seq;
   DevBuf rcodes;                   // K3a row code offsets (kern::k_rev_codes) for rcodes_lpad
   uint32_t rcodes_lpad = 0;
+  DevBuf fcodes;                   // k_score_pair's forward row code offsets (kern::k_fwd_codes)
+  uint32_t fcodes_lpad = 0;
   uint32_t nseq = 0, L = 0;
   DevBuf group_first, group_last;  // name groups (device merge)
   uint32_t ngroups = 0;
@@ -142,7 +144,8 @@ struct DeviceModule::Impl {
     bool valid = false;
     uint64_t cand_begin = 0, n = 0;
     uint32_t count = 0, per_block = 0;
-    bool swar = false, unit = false;  // the encoding they were built for; the kernel they chose
+    bool swar = false;  // the encoding they were built for
+    int kind = kScoreRows;  // the kernel they chose (score_tasks.h ScoreKind)
     int buf = 0;
   } prepared;
   struct ScoreState {                       // the launched, not yet finished K2
@@ -318,6 +321,9 @@ void DeviceModule::Bind(int device) {
   GHOSTM_SCAN_ATTRP(32, true) GHOSTM_SCAN_ATTRP(32, false) GHOSTM_SCAN_ATTRP(16, true)
   GHOSTM_SCAN_ATTRP(16, false) GHOSTM_SCAN_ATTRP(8, true) GHOSTM_SCAN_ATTRP(8, false)
 #undef GHOSTM_SCAN_ATTRP
+  for (const void *f : {(const void *)kern::k_score_pair<32>, (const void *)kern::k_score_pair<16>,
+                        (const void *)kern::k_score_pair<8>})
+    HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kern::kPairK2Words * 4)));
 #undef GHOSTM_SCAN_ATTR2
 #undef GHOSTM_SCAN_ATTR
   {
@@ -460,6 +466,7 @@ void DeviceModule::Free(DevQuery *q) {
   if (!q) return;
   q->seq.Release();
   q->rcodes.Release();
+  q->fcodes.Release();
   q->group_first.Release();
   q->group_last.Release();
   delete q;
@@ -944,14 +951,19 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
   // kernel where its blocks are not too many more): prepared for this range by
   // the previous launch (uploaded on the copy stream into the other task
   // buffer), else built and uploaded here
-  bool unit = false;
+  int kind = kScoreRows;
   int buf = -1;
   size_t ntasks = 0;
+  // staging and task buffers hold ScoreTaskBound tasks, or n pair entries
+  auto task_bytes = [&](uint64_t cn, uint32_t q0, uint32_t q1) {
+    return std::max<size_t>(ScoreTaskBound(cn, q0, q1, per_block, kern::kScoreQmaxUnit) * sizeof(kern::ScoreTask),
+                            (size_t)cn * 4);
+  };
   if (I.prepared.valid && I.prepared.cand_begin == cand_begin && I.prepared.n == n &&
       I.prepared.per_block == per_block && I.prepared.swar == swar) {
     buf = I.prepared.buf;
     ntasks = I.prepared.count;
-    unit = I.prepared.unit;
+    kind = I.prepared.kind;
     HIP_CHECK(hipStreamWaitEvent(S(stream_), I.ev_tasks, 0));
   }
   const bool stale = I.prepared.valid;  // an upload nothing will use may still read its staging
@@ -962,26 +974,35 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
     // page-locked staging per task buffer: this one's last upload was read by
     // a launch that has been waited for, so the copy needs no wait either
     PinnedBuf &hs = I.h_tasks[buf];
-    hs.Reserve(ScoreTaskBound(n, q_first, q_end, per_block, kern::kScoreQmaxUnit) * sizeof(kern::ScoreTask));
+    hs.Reserve(task_bytes(n, q_first, q_end));
     ntasks = BuildTasks(swar, cand_begin, n, q_first, q_end, counts, offsets, per_block, hs.as<kern::ScoreTask>(),
-                        &unit);
+                        &kind);
     TraceMark("tasks", ntasks);
     if (const char *dump = getenv("GHOSTM_DEBUG_TASKS")) {  // diagnostics: the launch's tasks and counts
       if (FILE *f = fopen(dump, "ab")) {
-        const uint64_t hdr[6] = {cand_begin, n, q_first, q_end, (uint64_t)unit, (uint64_t)ntasks};
+        const uint64_t hdr[6] = {cand_begin, n, q_first, q_end, (uint64_t)kind, (uint64_t)ntasks};
         fwrite(hdr, 8, 6, f);
-        fwrite(hs.p, sizeof(kern::ScoreTask), ntasks, f);
+        fwrite(hs.p, kind == kScorePairs ? 4 : sizeof(kern::ScoreTask), ntasks, f);
         fwrite(counts.data() + q_first, 4, q_end - q_first, f);
         fwrite(offsets.data() + q_first, 8, q_end - q_first, f);
         fclose(f);
       }
     }
-    const size_t tb = ntasks * sizeof(kern::ScoreTask);
+    const size_t tb = ntasks * (kind == kScorePairs ? 4 : sizeof(kern::ScoreTask));
     I.task_buf[buf].Reserve(tb);
     HIP_CHECK(hipMemcpyAsync(I.task_buf[buf].p, hs.p, tb, hipMemcpyHostToDevice, S(stream_)));
     TraceMark("tasks_up", ntasks);
   }
   I.task_turn = 1 - buf;
+  const bool unit = kind == kScoreUnit, pairs = kind == kScorePairs;
+  if (pairs && q->fcodes_lpad != lay.Lpad) {  // the query chunk's forward row codes, once
+    q->fcodes.Reserve((size_t)q->nseq * lay.Lpad + 16);
+    const size_t words = (size_t)q->nseq * (lay.Lpad / 4);
+    if (words)
+      hipLaunchKernelGGL(kern::k_fwd_codes, dim3((uint32_t)((words + 255) / 256)), dim3(256), 0, S(stream_),
+                         q->seq.as<uint8_t>(), q->nseq, q->L, lay.Lpad, q->fcodes.as<uint32_t>());
+    q->fcodes_lpad = lay.Lpad;
+  }
   I.score_out.Reserve(n * 4);
   I.end_out.Reserve(n * 4);
   kern::ScoreArgs a{};
@@ -1006,6 +1027,11 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
   a.out_base = cand_begin;
   a.swar_low = (uint32_t)swar_low;
   a.swar_restart = (uint32_t)swar_restart;
+  if (pairs) {
+    a.pairs = I.task_buf[buf].as<uint32_t>();
+    a.npairs = (uint32_t)ntasks;
+    a.fcodes = q->fcodes.as<uint32_t>();
+  }
   // counters: [0] cells (u64), [2] guard count (u32)
   I.counters.Reserve(32);
   HIP_CHECK(hipMemsetAsync(I.counters.p, 0, 32, S(stream_)));
@@ -1023,7 +1049,18 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
                               : (size_t)kern::kScoreQmax * kern::kProfRows * (lay.Lpad + 4) * 4;
   HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
   const dim3 grid((uint32_t)ntasks), block(kern::kScoreBlock);
-  if (packed) {
+  if (pairs) {
+    // persistent: one 768-thread workgroup per CU (the pair table), looping over the pairs
+    const uint32_t per_wg = (kern::kPairBlock / 64) * lay.gpw;
+    const dim3 pgrid(std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)I.cus, (uint32_t)((ntasks + per_wg - 1) / per_wg))));
+    const dim3 pblock(kern::kPairBlock);
+    const size_t plds = (size_t)kern::kPairK2Words * 4;
+    switch (lay.S) {
+      case 32: hipLaunchKernelGGL((kern::k_score_pair<32>), pgrid, pblock, plds, S(stream_), a); break;
+      case 16: hipLaunchKernelGGL((kern::k_score_pair<16>), pgrid, pblock, plds, S(stream_), a); break;
+      default: hipLaunchKernelGGL((kern::k_score_pair<8>), pgrid, pblock, plds, S(stream_), a); break;
+    }
+  } else if (packed) {
     switch (lay.S) {
       case 32:
         if (unit) hipLaunchKernelGGL((kern::k_score16f<32, true, true>), grid, block, lds, S(stream_), a);
@@ -1062,6 +1099,7 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
   times_.score_launches_framed += framed ? 1 : 0;
   times_.score_launches_swar += swar ? 1 : 0;
   times_.score_launches_unit += unit ? 1 : 0;
+  times_.score_launches_pair += pairs ? 1 : 0;
   P.active = true;
   P.guarded = half && guard;
   P.cand_begin = cand_begin;
@@ -1075,16 +1113,15 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
   if (next && next->n) {
     const int nb = I.task_turn;
     PinnedBuf &hs = I.h_tasks[nb];
-    bool nunit = false;
-    hs.Reserve(ScoreTaskBound(next->n, next->q_first, next->q_end, per_block, kern::kScoreQmaxUnit) *
-               sizeof(kern::ScoreTask));
+    int nkind = kScoreRows;
+    hs.Reserve(task_bytes(next->n, next->q_first, next->q_end));
     const size_t nt = BuildTasks(swar, next->cand_begin, next->n, next->q_first, next->q_end, counts, offsets,
-                                 per_block, hs.as<kern::ScoreTask>(), &nunit);
-    I.task_buf[nb].Reserve(nt * sizeof(kern::ScoreTask));
-    HIP_CHECK(hipMemcpyAsync(I.task_buf[nb].p, hs.p, nt * sizeof(kern::ScoreTask), hipMemcpyHostToDevice,
-                             S(copy_stream_)));
+                                 per_block, hs.as<kern::ScoreTask>(), &nkind);
+    const size_t nbytes = nt * (nkind == kScorePairs ? 4 : sizeof(kern::ScoreTask));
+    I.task_buf[nb].Reserve(nbytes);
+    HIP_CHECK(hipMemcpyAsync(I.task_buf[nb].p, hs.p, nbytes, hipMemcpyHostToDevice, S(copy_stream_)));
     HIP_CHECK(hipEventRecord(I.ev_tasks, S(copy_stream_)));
-    I.prepared = Impl::Prepared{true, next->cand_begin, next->n, (uint32_t)nt, per_block, swar, nunit, nb};
+    I.prepared = Impl::Prepared{true, next->cand_begin, next->n, (uint32_t)nt, per_block, swar, nkind, nb};
   }
 }
 

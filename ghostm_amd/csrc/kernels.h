@@ -1142,6 +1142,12 @@ struct ScoreArgs {
   // k_score16f<S, true> (integer patterns): the frame base before a window's
   // first END and the restart value at every END (host: ScoreSwarFrame)
   uint32_t swar_low, swar_restart;
+  // k_score_pair: candidate pairs of one query each (local index of the first
+  // candidate, bit 31 = no second), and every query's row codes in forward
+  // order (k_fwd_codes: Lpad / 4 words per query, code * 4 per byte)
+  const uint32_t *pairs;
+  uint32_t npairs;
+  const uint32_t *fcodes;
 };
 
 template <int S>
@@ -2066,6 +2072,253 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
   }
   WaveAddCells(a.cells, (in_group && i == 0) ? (unsigned long long)((vA ? ncolsA : 0u) + (vB ? ncolsB : 0u)) * a.L
                                              : 0ull);
+}
+
+// ------------------------------------------------------------------ K2 sparse
+// K2 for segments with few candidates per query (cfg 2: ~9): k_score16f's
+// per-block query profiles are not amortised there (four queries' profiles
+// built for ~37 candidates, one busy wave per block), so this kernel reads the
+// profile values from a query-independent pair table instead, as K3a's scan
+// does: word (a, b, q) = (v(q, a), v(q, b)), the two halves the 16-bit profile
+// rows of k_score16f<S, true> hold for query code q against DB codes a and b
+// (M + ext_pen, END = swar_restart, the fill code and padding rows the drop).
+// A lane group's two candidates are of one query (host pairs, BuildScorePairs),
+// so one ds_read_b32 at (pair of this column's codes, row's query code) gives
+// both halves of a row's diagonal term; the DP, the END handling and the end
+// column are k_score16f<S, true>'s. One 768-thread workgroup per CU (the
+// 96 KB table) loops over the pairs.
+constexpr uint32_t kPairK2Codes = 27;  // DB codes 0..25 and kFillCode (26)
+constexpr uint32_t kPairK2Stride = 33;  // dwords per (a, b) code pair: odd, as K3a's kPairStride
+constexpr uint32_t kPairK2Words = kPairK2Codes * kPairK2Codes * kPairK2Stride;
+constexpr int kPairBlock = 768;
+constexpr uint32_t kPairSingle = kPairSingleBit;  // pair entry: no second candidate
+
+// Per query, the byte offsets (code * 4) of its rows in forward order (row r
+// = query position r - pad; padding rows kPadCode), four per word.
+__global__ void k_fwd_codes(const uint8_t *qseq, uint32_t nq, uint32_t L, uint32_t Lpad, uint32_t *out) {
+  GHOSTM_POISON_LDS();
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t words = Lpad / 4, pad = Lpad - L;
+  if (t >= (size_t)nq * words) return;
+  const size_t q = t / words;
+  const uint32_t w = (uint32_t)(t - q * words);
+  uint32_t word = 0;
+  for (uint32_t v = 0; v < 4; ++v) {
+    const uint32_t r = 4 * w + v;
+    word |= (r >= pad ? (uint32_t)qseq[q * L + (r - pad)] * 4 : kPadCode * 4) << (8 * v);
+  }
+  out[t] = word;
+}
+
+template <int S>
+__global__ __launch_bounds__(kPairBlock) void k_score_pair(ScoreArgs a) {
+  GHOSTM_POISON_LDS();
+  using C = Cells<true>;
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_pk2[];
+  const int extp = -a.ext;
+  {
+    const uint32_t drop = (uint32_t)(0x10000u - (a.swar_low - 64u)) & 0xFFFFu;
+    auto enc = [&](uint32_t q, uint32_t c) -> uint32_t {  // BuildProfile16<C, true, true>'s value
+      if (c == kSeqEnd) return a.swar_restart;
+      if (q == kPadCode || c > kSeqEnd) return drop;
+      return (uint32_t)(a.mat[c * 32 + q] + extp) & 0xFFFFu;
+    };
+    for (uint32_t e = threadIdx.x; e < kPairK2Words; e += kPairBlock) {
+      const uint32_t pr = e / kPairK2Stride, q = e - pr * kPairK2Stride;
+      const uint32_t ca = pr / kPairK2Codes, cb = pr - ca * kPairK2Codes;
+      s_pk2[e] = q < 32 ? enc(q, ca) | enc(q, cb) << 16 : 0u;
+    }
+  }
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t g = lane / a.G, i = lane - g * a.G;
+  const bool in_group = g < a.gpw;
+  const uint32_t stride = gridDim.x * (kPairBlock / 64) * a.gpw;
+  const uint8_t *dbp = a.db - kDbFrontPad;
+  const uint32_t back = kDbFrontPad + a.dblen;
+  const __amdgpu_buffer_rsrc_t dbr = __builtin_amdgcn_make_buffer_rsrc((void *)dbp, 0, 0x7FFFFFFF, 0x00020000);
+  const uint32_t EXTP = (uint32_t)extp * 0x10001u;
+  const uint32_t KOE32 = (uint32_t)((a.open - a.ext) * 65537);
+  const uint32_t NEXT32 = (uint32_t)(a.ext * 65537);
+  const uint32_t ONE = 0x00010001u;
+  const uint32_t RESTART = a.swar_restart * 0x10001u;
+  const uint32_t steps = a.base + a.G - 1;
+  for (uint32_t first = (blockIdx.x * (kPairBlock / 64) + wave) * a.gpw; first < a.npairs; first += stride) {
+    const uint32_t p = first + g;
+    const bool valid = in_group && p < a.npairs;
+    const uint32_t pe = valid ? a.pairs[p] : kPairSingle;
+    const bool vA = valid, vB = valid && !(pe & kPairSingle);
+    const unsigned long long cA = a.out_base + (pe & ~kPairSingle), cB = cA + 1;
+    uint32_t offA = 0, offB = 0, wA = 0, wB = 0, q = 0;
+    if (vA) {
+      q = a.cand_qid[cA];
+      const int o = (int)(a.cand_start[cA] - a.extend);
+      offA = o < 0 ? 0u : (uint32_t)o;
+      wA = a.base;
+      if (offA + wA > a.dblen) wA = a.dblen - offA;
+    }
+    if (vB) {
+      const int o = (int)(a.cand_start[cB] - a.extend);
+      offB = o < 0 ? 0u : (uint32_t)o;
+      wB = a.base;
+      if (offB + wB > a.dblen) wB = a.dblen - offB;
+    }
+    // the rows' table offsets (code * 4), each in a register of its own
+    uint32_t roff[S];
+    {
+      const uint32_t *rw = a.fcodes + (size_t)q * (a.Lpad / 4) + i * (S / 4);
+      uint32_t qoff[S / 4];
+      if constexpr (S >= 16) {
+#pragma unroll
+        for (int w = 0; w < S / 16; ++w) {
+          const uint4 v = reinterpret_cast<const uint4 *>(rw)[w];
+          qoff[4 * w] = v.x;
+          qoff[4 * w + 1] = v.y;
+          qoff[4 * w + 2] = v.z;
+          qoff[4 * w + 3] = v.w;
+        }
+      } else {
+        const uint2 v = *reinterpret_cast<const uint2 *>(rw);
+        qoff[0] = v.x;
+        qoff[1] = v.y;
+      }
+#pragma unroll
+      for (int u = 0; u < S; ++u) {
+        roff[u] = (qoff[u >> 2] >> (8 * (u & 3))) & 0xFFu;
+        asm volatile("" : "+v"(roff[u]));
+      }
+    }
+    const uint32_t xA = (vA ? offA + kDbFrontPad : back) - i, xB = (vB ? offB + kDbFrontPad : back) - i;
+    // k_score16f<S, true>'s frame (integer patterns), from here on unchanged
+    uint32_t sig = (a.swar_low + ((int)a.G - (int)i) * extp) * 0x10001u;
+    const uint32_t sig_prev = (a.swar_low + ((int)a.G - (int)i - 1) * extp) * 0x10001u;
+    uint32_t H[S], E[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) { H[k] = sig_prev; E[k] = sig; }
+    uint32_t seen = 0, best = 0, col = (i & 0xFFFFu) * 0x10001u, mreg = ONE;
+    uint32_t hout = sig_prev, fout = 0, hprev = sig_prev;
+    uint32_t c0A = dbp[xA], c0B = dbp[xB], c1A = dbp[xA + 1], c1B = dbp[xB + 1];
+    const uint32_t wA_ = vA ? wA : 0u, wB_ = vB ? wB : 0u;
+    const char *const tab = reinterpret_cast<const char *>(s_pk2);
+    auto column = [&](uint32_t step, auto tested_c, auto fill_c) {
+      constexpr bool tested = decltype(tested_c)::value, in_fill = decltype(fill_c)::value;
+      uint32_t hin = ShiftUp(hout), fin = ShiftUp(fout);
+      uint32_t rA = c0A, rB = c0B;
+      uint32_t fillm = 0;
+      if constexpr (tested) {
+        const uint32_t j = step - i;
+        rA = j < wA_ ? rA : kSeqEnd;
+        rB = j < wB_ ? rB : kSeqEnd;
+        if constexpr (in_fill) {
+          fillm = (int)j < 0 ? 0xFFFFFFFFu : 0u;
+          rA = fillm ? kFillCode : rA;
+          rB = fillm ? kFillCode : rB;
+        }
+      }
+      c0A = c1A;
+      c0B = c1B;
+      c1A = __builtin_amdgcn_raw_buffer_load_b8(dbr, xA, step + 2, 0);
+      c1B = __builtin_amdgcn_raw_buffer_load_b8(dbr, xB, step + 2, 0);
+      auto end_mask = [&]() {
+        uint32_t e = PkSign(PkAddU16(rA | (rB << 16), 0x7FE77FE7u));
+        if constexpr (in_fill) e &= ~fillm;
+        return e;
+      };
+      uint32_t end = 0;
+      bool any_end;
+      if constexpr (!tested) {
+        any_end = __builtin_amdgcn_ballot_w64(max((uint16_t)rA, (uint16_t)rB) >= (uint16_t)kSeqEnd) != 0;
+        if (any_end) end = end_mask();
+      } else {
+        end = end_mask();
+        any_end = __builtin_amdgcn_ballot_w64(end != 0) != 0;
+      }
+      const bool quiet = !tested && !any_end;
+      uint32_t sigc = sig;
+      mreg = ONE;
+      if (any_end) {
+        sigc = BfiV(end, RESTART, sig);
+        mreg = ONE & ~end;
+        const uint32_t reset = end & seen;
+        seen |= end;
+        if (__builtin_amdgcn_ballot_w64(reset != 0)) {
+#pragma unroll
+          for (int k = 0; k < S; ++k) E[k] = BfiV(reset, 0u, E[k]);
+        }
+      }
+      if (i == 0) { hin = sigc; fin = 0; }
+      const uint32_t diag0 = hprev;
+      hprev = hin;
+      const uint32_t zn = sigc + EXTP;
+      const hf2 Z1 = HF(zn);
+      const char *tp = tab + MadU24(rA, kPairK2Codes * kPairK2Stride * 4, MulU24(rB, kPairK2Stride * 4));
+      auto T = [&](int u) { return *reinterpret_cast<const uint32_t *>(tp + roff[u]); };
+      auto dsum = [&](uint32_t h, uint32_t p) -> uint32_t { return W(U2(h) * U2(mreg) + U2(p)); };
+      uint32_t diag = diag0, F = fin, cm = sigc;
+#pragma unroll
+      for (int k = 0; k < S; k += 8) {
+        uint32_t tw[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) tw[u] = T(k + u);
+        uint32_t s[8];
+        s[0] = dsum(diag, tw[0]);
+        s[1] = dsum(H[k], tw[1]);
+        diag = H[k + 7];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const hf2 h = __builtin_elementwise_maximum(__builtin_elementwise_maximum(HF(s[u]), HF(E[k + u])), HF(F));
+          H[k + u] = W(h);
+          const hf2 oE = HF(W(h) + KOE32);
+          if (u + 2 < 8) s[u + 2] = dsum(H[k + u + 1], tw[u + 2]);
+          const hf2 Gm = __builtin_elementwise_maximum(HF(F), oE);
+          E[k + u] = W(__builtin_elementwise_maximum(__builtin_elementwise_maximum(HF(E[k + u]), oE), Z1));
+          F = W(Gm) + NEXT32;
+        }
+        cm = C::Max3(C::Max3(H[k], H[k + 1], H[k + 2]), C::Max3(H[k + 3], H[k + 4], H[k + 5]),
+                     C::Max3(H[k + 6], H[k + 7], cm));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      hout = H[S - 1];
+      fout = F;
+#pragma unroll
+      for (int k = 0; k < S; ++k) asm("" : "+v"(E[k]));
+      const uint32_t cmr = W(U2(cm) - U2(sigc));
+      uint32_t keep = PkSign(PkSubI16(cmr, best));
+      if (!quiet) keep |= end | fillm;
+      best = BfiV(keep, best, cmr);
+      col = BfiVS(keep, col, __builtin_amdgcn_readfirstlane(step * 0x10001u));
+      sig = zn;
+    };
+    const uint32_t fill = min(a.G - 1, steps);
+    uint32_t step = 0;
+    for (; step < fill; ++step) column(step, std::true_type{}, std::true_type{});
+    for (; step + 1 < a.base; step += 2) {
+      column(step, std::false_type{}, std::false_type{});
+      column(step + 1, std::false_type{}, std::false_type{});
+    }
+    for (; step < a.base; ++step) column(step, std::false_type{}, std::false_type{});
+    for (; step < steps; ++step) column(step, std::true_type{}, std::false_type{});
+    int BA = (int)(best & 0xFFFFu), CA = (int)(((col & 0xFFFFu) - i) & 0xFFFFu);
+    int BB = (int)(best >> 16), CB = (int)(((col >> 16) - i) & 0xFFFFu);
+    for (uint32_t k = 1; k < a.G; ++k) {
+      const int src = (int)(g * a.G + k);
+      const int oba = __shfl(BA, src), oca = __shfl(CA, src);
+      const int obb = __shfl(BB, src), ocb = __shfl(CB, src);
+      if (oba > BA || (oba == BA && oca > CA)) { BA = oba; CA = oca; }
+      if (obb > BB || (obb == BB && ocb > CB)) { BB = obb; CB = ocb; }
+    }
+    if (i == 0) {
+      if (vA) {
+        a.score_out[cA - a.out_base] = (uint32_t)BA;
+        a.end_out[cA - a.out_base] = offA + (uint32_t)CA;
+      }
+      if (vB) {
+        a.score_out[cB - a.out_base] = (uint32_t)BB;
+        a.end_out[cB - a.out_base] = offB + (uint32_t)CB;
+      }
+    }
+    WaveAddCells(a.cells, (in_group && i == 0) ? (unsigned long long)(wA_ + wB_) * a.L : 0ull);
+  }
 }
 
 // ------------------------------------------------------------------ K3 traceback

@@ -8,6 +8,7 @@ namespace kern {
 
 constexpr int kScoreQmax = 4;       // query profiles per K2 block (16-bit rows)
 constexpr int kScoreQmaxUnit = 2;   // k_score16f UNIT: 32-bit profile words, half the queries per block
+constexpr uint32_t kPairSingleBit = 0x80000000u;  // k_score_pair entry: a pair without its second candidate
 
 struct ScoreTask {
   unsigned long long begin;  // first candidate (global index)

@@ -263,6 +263,30 @@ inline void CountTasks(uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32
   *np = full + PairedFromRemainders(rem, per_block);
 }
 
+// Sparse segments (k_score_pair): each query's candidates in pairs, the local
+// index (from cand_begin) of a pair's first candidate, kPairSingle set when it
+// has no second (a query's odd last one). Returns the number of pairs; `out`
+// has room for n entries.
+inline size_t BuildScorePairs(uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32_t q_end,
+                              const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets,
+                              uint32_t *out) {
+  size_t np = 0;
+  const uint64_t cand_end = cand_begin + n;
+  for (uint32_t qi = q_first; qi < q_end; ++qi) {
+    const uint64_t lo = std::max<uint64_t>(offsets[qi], cand_begin);
+    const uint64_t hi = std::min<uint64_t>(offsets[qi] + counts[qi], cand_end);
+    for (uint64_t c = lo; c < hi; c += 2)
+      out[np++] = (uint32_t)(c - cand_begin) | (c + 1 < hi ? 0u : kern::kPairSingleBit);
+  }
+  return np;
+}
+
+// Which K2 kernel runs a segment (ScoreKind) and its work list.
+enum ScoreKind { kScoreRows = 0, kScoreUnit = 1, kScorePairs = 2 };
+// below this many candidates per query the pair-table kernel runs (cfg 2: ~9
+// per query; GHOSTM_K2_PAIR_MAX overrides, GHOSTM_K2=pair forces it)
+constexpr uint64_t kScorePairMax = 0;  // (off until measured on the GPU)
+
 // The K2 tasks of a segment, and which kernel runs them (GHOSTM_K2=unit|swar16
 // and GHOSTM_K2_TASKS=paired|consecutive force a choice). With 16-bit integer
 // patterns (swar) the unit-pair kernel is used where its blocks, each ~7 %
@@ -273,15 +297,25 @@ inline void CountTasks(uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32
 // counts the runs measured faster (cfg 4: 19.0 against 19.5 ms per launch),
 // at 63 candidates per query the pairs (cfg 3: 4.83 against 5.57 ms, 14 %
 // fewer blocks). Only the chosen list is built; the others are counted.
-// `out` has room for ScoreTaskBound(...) tasks.
+// Below kScorePairMax candidates per query (and with integer patterns) the
+// segment runs k_score_pair over BuildScorePairs' list instead, written into
+// `out` as uint32 entries. `out` has room for ScoreTaskBound(...) tasks and n
+// uint32 entries.
 inline size_t BuildTasks(bool swar, uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32_t q_end,
                          const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets,
-                         uint32_t per_block, kern::ScoreTask *out, bool *unit_out) {
+                         uint32_t per_block, kern::ScoreTask *out, int *kind_out) {
   const char *k2 = getenv("GHOSTM_K2");
   const char *how = getenv("GHOSTM_K2_TASKS");
   const bool force_unit = k2 && strcmp(k2, "unit") == 0, force_rows = k2 && strcmp(k2, "swar16") == 0;
+  const bool force_pair = k2 && strcmp(k2, "pair") == 0;
   bool unit = false, paired = false;
   const uint64_t per_query = n / std::max<uint32_t>(1, q_end - q_first);
+  uint64_t pair_max = kScorePairMax;
+  if (const char *e = getenv("GHOSTM_K2_PAIR_MAX")) pair_max = strtoull(e, nullptr, 10);
+  if (swar && q_end > q_first && !force_unit && !force_rows && !how && (force_pair || per_query < pair_max)) {
+    *kind_out = kScorePairs;
+    return BuildScorePairs(cand_begin, n, q_first, q_end, counts, offsets, reinterpret_cast<uint32_t *>(out));
+  }
   if (swar && q_end > q_first && !force_rows && !how && !force_unit && per_query >= 96) {
     unit = true;  // dense (cfg 4: 127 per query): runs of two queries fill their blocks, no count needed
   } else if (swar && q_end > q_first && !force_rows && (how || force_unit || per_query >= 24)) {
@@ -296,7 +330,7 @@ inline size_t BuildTasks(bool swar, uint64_t cand_begin, uint64_t n, uint32_t q_
       fprintf(stderr, "k2 tasks: %llu candidates, %u queries: consecutive(2) %zu, paired %zu, consecutive(4) %zu -> %s\n",
               (unsigned long long)n, q_end - q_first, nc, np, n4, unit ? (paired ? "unit paired" : "unit consecutive") : "rows");
   }
-  *unit_out = unit;
+  *kind_out = unit ? kScoreUnit : kScoreRows;
   if (unit && paired) return BuildScoreTasksPaired(cand_begin, n, q_first, q_end, counts, offsets, per_block, out);
   return BuildScoreTasks(cand_begin, n, q_first, q_end, counts, offsets, per_block,
                          unit ? kern::kScoreQmaxUnit : kern::kScoreQmax, out);

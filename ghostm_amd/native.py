@@ -80,6 +80,7 @@ class GhostmStats(ctypes.Structure):
         ("score_launches_unit", c_uint64),
         ("traceback_launches_strips", c_uint64),
         ("seconds_traceback_scan", ctypes.c_double),
+        ("score_launches_pair", c_uint64),
     ]
 
     def as_dict(self) -> dict:

@@ -206,6 +206,7 @@ typedef struct GhostmStats {
   uint64_t traceback_launches_strips; /* K3 key DPs run by strip class (each hit on the strips up to its first maximal cell) */
   double seconds_traceback_scan;    /* of seconds_traceback: the scan phase (k_tb_prep, k_tb_pairs, the sorts,
                                        k_tb_scan); the rest is the key DP (k_traceback_key) */
+  uint64_t score_launches_pair;     /* K2 launches of sparse segments run by the pair-table kernel (k_score_pair) */
 } GhostmStats;
 
 /* Session: parse `aln` options exactly like the reference (getopt string

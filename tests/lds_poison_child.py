@@ -5,8 +5,9 @@ Runs with GHOSTM_LIB_PATH = the LDS poison build (libghostm_hip_poison.so: every
 kernel fills its whole LDS allocation with GHOSTM_LDS_POISON_PATTERN before its
 own code) and checks the golden variants under the kernel forms that read LDS:
 
-  golden:  every golden variant with the default kernels and with the unit-pair
-           K2 forced as paired and as consecutive tasks;
+  golden:  every golden variant with the default kernels, with the unit-pair
+           K2 forced as paired and as consecutive tasks, and with the sparse
+           segments' pair-table K2 forced;
   kernels: every K3 scan mode, every K4 mode, every K1 size class and the
            offset pass (class caps at the dataset's quartiles, slot cap 2), and
            the many-segment device pipeline.
@@ -55,6 +56,7 @@ def plan(group):
             yield ds, var, opts, dict(env), "default"
             for tasks in ("paired", "consecutive"):
                 yield ds, var, opts, dict(env, GHOSTM_K2="unit", GHOSTM_K2_TASKS=tasks), f"unit_{tasks}"
+            yield ds, var, opts, dict(env, GHOSTM_K2="pair"), "pair"
         return
     scan_sets = [("syn_small", "default", []), ("syn_dna", "default", []), ("syn_chunks", "default", []),
                  ("protein_testset", "y2", ["-y", "2"]),

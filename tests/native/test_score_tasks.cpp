@@ -2,7 +2,9 @@
 // every candidate of the segment is in exactly one task, each task's candidates
 // belong to the queries whose profiles it builds (the unit kernel reads a task
 // as two ranges, the others as one consecutive run over q_first..), and no
-// task exceeds a workgroup.
+// task exceeds a workgroup. The sparse kernel's pair lists: every candidate in
+// exactly one pair, both candidates of a pair of one query, the single flag
+// only on a query's odd last candidate.
 #include <cstdio>
 #include <random>
 #include <vector>
@@ -44,6 +46,27 @@ static int Check(const char *what, const std::vector<ScoreTask> &tasks, size_t n
   return 0;
 }
 
+static int CheckPairs(const uint32_t *pairs, size_t np, uint64_t cand_begin, uint64_t n,
+                      const std::vector<uint32_t> &qid_of) {
+  std::vector<int> seen(n, 0);
+  for (size_t k = 0; k < np; ++k) {
+    const bool single = pairs[k] & ghostm::kern::kPairSingleBit;
+    const uint64_t a = pairs[k] & ~ghostm::kern::kPairSingleBit;
+    if (a >= n || (!single && a + 1 >= n)) { printf("pair %zu outside the segment\n", k); return 1; }
+    if (seen[a]++) { printf("pair %zu: candidate twice\n", k); return 1; }
+    if (!single) {
+      if (seen[a + 1]++) { printf("pair %zu: second candidate twice\n", k); return 1; }
+      if (qid_of[cand_begin + a] != qid_of[cand_begin + a + 1]) { printf("pair %zu spans two queries\n", k); return 1; }
+    } else if (a + 1 < n && qid_of[cand_begin + a] == qid_of[cand_begin + a + 1]) {
+      printf("pair %zu single though its query has a next candidate\n", k);
+      return 1;
+    }
+  }
+  for (uint64_t c = 0; c < n; ++c)
+    if (!seen[c]) { printf("pairs: candidate %llu missing\n", (unsigned long long)c); return 1; }
+  return 0;
+}
+
 int main() {
   std::mt19937_64 rng(7);
   const uint32_t per_block = 128, wave_slots = 32;
@@ -70,10 +93,17 @@ int main() {
     while (q0 < nq && offsets[q0] + counts[q0] <= b) ++q0;
     while (q1 > 0 && offsets[q1 - 1] >= e) --q1;
     const uint64_t n = e - b;
-    for (int mode = 0; mode < 4; ++mode) {
+    for (int mode = 0; mode < 5; ++mode) {
       const bool unit = true;
       const uint32_t qmax = 2;
-      std::vector<ScoreTask> tasks(ghostm::ScoreTaskBound(n, q0, q1, per_block, qmax));
+      // room for the bound's tasks and for n pair entries
+      std::vector<ScoreTask> tasks(std::max<size_t>(ghostm::ScoreTaskBound(n, q0, q1, per_block, qmax),
+                                                    n * 4 / sizeof(ScoreTask) + 1));
+      if (mode == 4) {  // the sparse kernel's pairs
+        const size_t np = ghostm::BuildScorePairs(b, n, q0, q1, counts, offsets, reinterpret_cast<uint32_t *>(tasks.data()));
+        if (CheckPairs(reinterpret_cast<const uint32_t *>(tasks.data()), np, b, n, qid_of)) return 1;
+        continue;
+      }
       size_t nt;
       const char *what;
       if (mode == 0) {
@@ -106,8 +136,15 @@ int main() {
           }
         }
         what = "chosen kernel";
-        bool unit_k = false;
-        nt = ghostm::BuildTasks(true, b, n, q0, q1, counts, offsets, per_block, tasks.data(), &unit_k);
+        int kind = -1;
+        nt = ghostm::BuildTasks(true, b, n, q0, q1, counts, offsets, per_block, tasks.data(), &kind);
+        if (kind == ghostm::kScorePairs) {  // sparse: fewer than kScorePairMax per query
+          if (n / std::max<uint32_t>(1, q1 - q0) >= ghostm::kScorePairMax) { printf("pairs chosen when dense\n"); return 1; }
+          if (CheckPairs(reinterpret_cast<const uint32_t *>(tasks.data()), nt, b, n, qid_of)) return 1;
+          ++trials;
+          continue;
+        }
+        const bool unit_k = kind == ghostm::kScoreUnit;
         if (Check(what, tasks, nt, unit_k, unit_k ? 2u : 4u, b, n, qid_of, per_block)) return 1;
         if (!unit_k && nt != ghostm::CountScoreTasks(b, n, q0, q1, counts, offsets, per_block, 4)) {
           printf("CountScoreTasks disagrees with BuildScoreTasks\n");

@@ -34,4 +34,4 @@ def test_golden_variants_under_lds_poison(pattern, group, data_root):
     assert lines, p.stderr[-3000:]
     res = json.loads(lines[-1])
     assert p.returncode == 0 and not res.get("failures") and not res.get("error"), res
-    assert res["runs"] >= (132 if group == "golden" else 50)
+    assert res["runs"] >= (176 if group == "golden" else 50)

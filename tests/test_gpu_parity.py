@@ -61,6 +61,22 @@ def test_gpu_unit_k2_matches_reference_golden(ds, var, opts, env, tasks, dataset
         assert st["score_launches_unit"] == st["score_launches"]
 
 
+@pytest.mark.parametrize("ds,var,opts,env", cases.VARIANTS, ids=[f"{v[0]}/{v[1]}" for v in cases.VARIANTS])
+def test_gpu_pair_k2_matches_reference_golden(ds, var, opts, env, dataset, golden, tmp_path):
+    """Every golden variant with the sparse segments' K2 forced at any density
+    (GHOSTM_K2=pair: k_score_pair, the pair-table kernel that runs segments of
+    fewer than 24 candidates per query by default): windows over one or several
+    subject ENDs, a window starting at an END, the DB's end, one-subject DBs,
+    S = 16 and 8, G = 1, odd candidate counts (single pairs), every gap setting."""
+    d = dataset(ds)
+    text, st = _gpu_text(d, opts, dict(env, GHOSTM_K2="pair"), str(tmp_path / "g.out"))
+    want = golden["aln"][f"{ds}/{var}"]
+    (tmp_path / "g.out").write_bytes(text)
+    assert cases.sha256(str(tmp_path / "g.out")) == want["sha256"]
+    if st["score_launches_swar"] == st["score_launches"] > 0:  # integer patterns fit: the pair kernel ran
+        assert st["score_launches_pair"] == st["score_launches"]
+
+
 @pytest.mark.parametrize("merge", ["device", "device_thread", "host"])
 @pytest.mark.parametrize("ds,var,opts,env", cases.BATCH_VARIANTS,
                          ids=[f"{v[0]}/{v[1]}" for v in cases.BATCH_VARIANTS])
@@ -224,8 +240,8 @@ def test_reference_gpu_batching_rule(dataset):
     lib.FreeGpu()
 
 
-@pytest.mark.parametrize("kind", ["int32", "int16", "f16plain", "f16frame", "swar16", "unit", "k2_nowait", "k3_int32",
-                                  "k3_nostrips", "k1_merge"])
+@pytest.mark.parametrize("kind", ["int32", "int16", "f16plain", "f16frame", "swar16", "unit", "pair", "k2_nowait",
+                                  "k3_int32", "k3_nostrips", "k1_merge"])
 @pytest.mark.parametrize("ds,var,opts", [("syn_small", "default", []), ("syn_short", "default", []),
                                          ("syn_small", "r64_pam250", ["-r", "64", "-M", cases.PAM250, "-y", "2"])])
 def test_forced_score_encoding_matches_golden(kind, ds, var, opts, dataset, golden, tmp_path):
@@ -257,6 +273,8 @@ def test_forced_score_encoding_matches_golden(kind, ds, var, opts, dataset, gold
         assert st["score_launches_swar"] == st["score_launches"] > 0 and st["score_launches_unit"] == 0
     elif kind == "unit":  # ... with unit-pair profile words (k_score16f<S, true, true>), however sparse
         assert st["score_launches_unit"] == st["score_launches"] > 0
+    elif kind == "pair":  # the pair-table kernel (k_score_pair), however dense
+        assert st["score_launches_pair"] == st["score_launches"] > 0
     else:
         assert st["score_launches"] > 0 and st["score_launches_half"] == 0
         assert st["score_launches_packed"] == (st["score_launches"] if kind == "int16" else 0)
