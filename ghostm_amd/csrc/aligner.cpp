@@ -1277,12 +1277,28 @@ struct LineFormat {
 };
 
 namespace {
-// Appends lines through a raw cursor into a part's text buffer.
+// Appends lines through a raw cursor into a part's text buffer. The write
+// position and its limit live in the cursor (registers), not in the buffer:
+// a line's byte stores may alias any object in memory, so a position read back
+// from the buffer after each line's stores cost the formatter half its speed
+// (a host microbenchmark of 40 K lines per thread: 16.5 against 8.5 ms).
 struct TextCursor {
   TextBuf &s;
-  explicit TextCursor(TextBuf &buf) : s(buf) {}
-  char *Reserve(size_t need) { return s.Reserve(need); }
-  void Commit(char *end) { s.Commit(end); }
+  char *cur, *lim;
+  explicit TextCursor(TextBuf &buf) : s(buf) {
+    cur = s.Reserve(0);
+    lim = cur + s.room();
+  }
+  char *Reserve(size_t need) {
+    if ((size_t)(lim - cur) < need) {
+      s.Commit(cur);
+      cur = s.Reserve(need);
+      lim = cur + s.room();
+    }
+    return cur;
+  }
+  void Commit(char *end) { cur = end; }
+  ~TextCursor() { s.Commit(cur); }
 };
 }  // namespace
 

@@ -77,6 +77,7 @@ class TextBuf {
 
   const char *data() const { return p_; }
   size_t size() const { return n_; }
+  size_t room() const { return cap_ - n_; }  // bytes writable at data() + size() without growing
   void clear() { n_ = 0; }
   void reserve(size_t cap) {
     if (cap <= cap_) return;

@@ -284,8 +284,10 @@ inline size_t BuildScorePairs(uint64_t cand_begin, uint64_t n, uint32_t q_first,
 // Which K2 kernel runs a segment (ScoreKind) and its work list.
 enum ScoreKind { kScoreRows = 0, kScoreUnit = 1, kScorePairs = 2 };
 // below this many candidates per query the pair-table kernel runs (cfg 2: ~9
-// per query; GHOSTM_K2_PAIR_MAX overrides, GHOSTM_K2=pair forces it)
-constexpr uint64_t kScorePairMax = 0;  // (off until measured on the GPU)
+// per query, K2 5.1 -> 3.4 ms per step, profiles/r5d/; at cfg 3's 63 per query
+// it lost to the unit kernel, 14.8 -> 18.4 ms; GHOSTM_K2_PAIR_MAX overrides,
+// GHOSTM_K2=pair forces it)
+constexpr uint64_t kScorePairMax = 16;
 
 // The K2 tasks of a segment, and which kernel runs them (GHOSTM_K2=unit|swar16
 // and GHOSTM_K2_TASKS=paired|consecutive force a choice). With 16-bit integer

@@ -28,6 +28,7 @@ int main() {
     t.Commit(p + len + 1);
   }
   check(t.size() == want.size() && std::string(t.data(), t.size()) == want, "grown text equals the appended lines");
+  check(t.room() >= 1 && t.Reserve(t.room()) == t.data() + t.size(), "room() bytes fit without growing");
   const char *before = t.data();
   t.clear();
   check(t.size() == 0, "clear empties");
