@@ -35,6 +35,12 @@ std::mutex g_trace_mu;
 std::vector<TraceEvent> g_trace;
 }  // namespace
 
+double ThreadCpuSeconds() {
+  timespec ts;
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
 bool TraceOn() {
   static const bool on = [] {
     const char *e = getenv("GHOSTM_TRACE");
@@ -1165,17 +1171,19 @@ constexpr uint32_t kIdLen = 512, kIdMatch = 128;
 // bytes. A hit copies the 16 bytes straight from the two loaded words into the
 // line (which has kFixed bytes of room) and steps on by the length: no reload
 // from a stack buffer at an odd offset, which stalled on store forwarding. The
-// storage comes zeroed from the OS (HostAlloc: huge pages when large), so a
-// table costs nothing until entries are used: the session's create -> run
-// path no longer formats 60 K identity strings up front.
+// storage comes zeroed from calloc (the OS's zero pages), so a table costs
+// nothing until entries are used: the session's create -> run path no longer
+// formats 60 K identity strings up front.
 struct TextCache {
   struct Entry {
     std::atomic<uint64_t> a, b;
   };
   Entry *e = nullptr;
   size_t n = 0;
-  explicit TextCache(size_t entries) : e(static_cast<Entry *>(HostAlloc(entries * sizeof(Entry)))), n(entries) {}
-  ~TextCache() { HostFree(e, n * sizeof(Entry)); }
+  explicit TextCache(size_t entries) : e(static_cast<Entry *>(std::calloc(entries, sizeof(Entry)))), n(entries) {
+    if (!e) throw std::bad_alloc();
+  }
+  ~TextCache() { std::free(e); }
   TextCache(const TextCache &) = delete;
   TextCache &operator=(const TextCache &) = delete;
   // the text of entry k, made by make(buf) (writes at most 15 bytes, returns its end) on first use
@@ -1277,28 +1285,17 @@ struct LineFormat {
 };
 
 namespace {
-// Appends lines through a raw cursor into a part's text buffer. The write
-// position and its limit live in the cursor (registers), not in the buffer:
-// a line's byte stores may alias any object in memory, so a position read back
-// from the buffer after each line's stores cost the formatter half its speed
-// (a host microbenchmark of 40 K lines per thread: 16.5 against 8.5 ms).
+// Appends lines through a raw cursor into a std::string that grows in chunks.
 struct TextCursor {
-  TextBuf &s;
-  char *cur, *lim;
-  explicit TextCursor(TextBuf &buf) : s(buf) {
-    cur = s.Reserve(0);
-    lim = cur + s.room();
-  }
+  std::string &s;
+  size_t used;
+  explicit TextCursor(std::string &str) : s(str), used(str.size()) {}
   char *Reserve(size_t need) {
-    if ((size_t)(lim - cur) < need) {
-      s.Commit(cur);
-      cur = s.Reserve(need);
-      lim = cur + s.room();
-    }
-    return cur;
+    if (s.size() < used + need) s.resize(std::max(used + need, s.size() * 2 + 4096));
+    return &s[used];
   }
-  void Commit(char *end) { cur = end; }
-  ~TextCursor() { s.Commit(cur); }
+  void Commit(char *end) { used = (size_t)(end - s.data()); }
+  ~TextCursor() { s.resize(used); }
 };
 }  // namespace
 
@@ -1310,8 +1307,8 @@ const LineFormat &Session::Format() {
 void Session::Part::Reset(size_t pieces) {
   text.resize(pieces);
   hits.resize(pieces);
-  for (TextBuf &t : text) t.clear();
-  for (HitVec &h : hits) h.clear();
+  for (std::string &t : text) t.clear();
+  for (std::vector<GhostmHit> &h : hits) h.clear();
 }
 
 Session::Part *Session::NewPart() {
@@ -1325,7 +1322,7 @@ void Session::FormatResults(const QueryData &q, const Results &results, Part *ou
   const LineFormat &w = Format();
   ParallelFor(n, threads_, [&](size_t b, size_t e, unsigned t) {
     TextCursor text(out->text[t]);
-    HitVec &hits = out->hits[t];
+    std::vector<GhostmHit> &hits = out->hits[t];
     for (size_t i = b; i < e; ++i) {
       const uint64_t space = (uint64_t)q.qlen[i] * (uint64_t)db_sum_u32_;
       const float scaled = (float)space * w.ev.p.K;
@@ -1350,8 +1347,20 @@ void Session::FormatSelected(const QueryData &q, uint32_t g0, const std::vector<
   const unsigned workers = std::max(1u, threads_ > 1 ? threads_ - 1 : 1u);
   out->Reset(workers);
   const LineFormat &w = Format();
+  // timeline diagnostics: each worker's wall and on-CPU time (a thread that
+  // waits for a CPU, e.g. under a cgroup quota, shows wall >> CPU)
+  const bool trace = TraceOn();
+  std::vector<double> wall(trace ? workers : 0), cpu(trace ? workers : 0);
   ParallelFor(ng, workers, [&](size_t b, size_t e, unsigned t) {
-    HitVec &ph = out->hits[t];
+    const double w0 = trace ? NowSeconds() : 0.0, c0 = trace ? ThreadCpuSeconds() : 0.0;
+    struct Done {
+      bool on;
+      double w0, c0, *wall, *cpu;
+      ~Done() {
+        if (on) *wall = NowSeconds() - w0, *cpu = ThreadCpuSeconds() - c0;
+      }
+    } done{trace, w0, c0, trace ? &wall[t] : nullptr, trace ? &cpu[t] : nullptr};
+    std::vector<GhostmHit> &ph = out->hits[t];
     size_t nh = 0;
     for (size_t g = b; g < e; ++g) nh += counts[g];
     out->text[t].reserve(nh * 96);
@@ -1375,6 +1384,13 @@ void Session::FormatSelected(const QueryData &q, uint32_t g0, const std::vector<
       }
     }
   });
+  if (trace) {
+    double ws = 0, cs = 0, wm = 0;
+    for (unsigned t = 0; t < workers; ++t) ws += wall[t], cs += cpu[t], wm = std::max(wm, wall[t]);
+    TraceMark("fmt_wall_max_us", (uint64_t)(wm * 1e6));
+    TraceMark("fmt_wall_sum_us", (uint64_t)(ws * 1e6));
+    TraceMark("fmt_cpu_sum_us", (uint64_t)(cs * 1e6));
+  }
 }
 
 void Session::Run(bool stream_to_file) {
@@ -1477,11 +1493,11 @@ const std::string &Session::Output() {
   if (!joined_valid_) {
     size_t n = 0;
     for (size_t k = 0; k < used_parts_; ++k)
-      for (const TextBuf &t : parts_[k].text) n += t.size();
+      for (const std::string &t : parts_[k].text) n += t.size();
     joined_.clear();
     joined_.reserve(n);
     for (size_t k = 0; k < used_parts_; ++k)
-      for (const TextBuf &t : parts_[k].text) joined_.append(t.data(), t.size());
+      for (const std::string &t : parts_[k].text) joined_.append(t);
     joined_valid_ = true;
   }
   return joined_;
@@ -1518,7 +1534,7 @@ size_t Session::DeviceHits(void *dst, size_t cap) {
 void Session::PartDone(const Part *part) {
   if (stream_fd_ < 0) return;
   writer_->Submit([this, part] {
-    for (const TextBuf &t : part->text) {
+    for (const std::string &t : part->text) {
       const char *p = t.data();
       size_t left = t.size();
       while (left && !stream_failed_) {
@@ -1546,12 +1562,12 @@ void Session::WriteOutputFile() {
   } done;
   // the pieces in output order, written at their offsets by parallel threads
   // (an unwritable path writes nothing, as the reference's unchecked ofstream)
-  std::vector<const TextBuf *> pieces;
+  std::vector<const std::string *> pieces;
   std::vector<uint64_t> at;
   uint64_t total = 0;
   for (size_t k = 0; k < used_parts_; ++k)
-    for (const TextBuf &t : parts_[k].text) {
-      if (!t.size()) continue;
+    for (const std::string &t : parts_[k].text) {
+      if (t.empty()) continue;
       pieces.push_back(&t);
       at.push_back(total);
       total += t.size();

@@ -20,7 +20,6 @@
 #include <vector>
 
 #include "../../include/ghostm_hip.h"
-#include "host_buffers.h"
 #include "device.h"
 #include "formats.h"
 #include "scoring.h"
@@ -169,12 +168,10 @@ class Session {
   };
   // Output of one segment: one piece per formatting worker, in output order.
   // Parts are reused across runs, so their buffers keep their capacity (no
-  // release and re-fault of ~100 bytes per hit on every run); a session's first
-  // run writes into huge-page mappings (host_buffers.h).
-  using HitVec = std::vector<GhostmHit, HostAllocator<GhostmHit>>;
+  // release and re-fault of ~100 bytes per hit on every run).
   struct Part {
-    std::vector<TextBuf> text;
-    std::vector<HitVec> hits;
+    std::vector<std::string> text;
+    std::vector<std::vector<GhostmHit>> hits;
     void Reset(size_t pieces);
   };
   using Results = std::vector<std::vector<HitRecord>>;

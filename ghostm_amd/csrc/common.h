@@ -33,6 +33,7 @@ inline double NowSeconds() {
 // GHOSTM_TRACE=1: a host timeline of each GhostmSessionRun (label, value,
 // thread, ms since the run started), printed to stderr when the run ends.
 bool TraceOn();
+double ThreadCpuSeconds();  // this thread's CPU time (CLOCK_THREAD_CPUTIME_ID)
 void TraceMark(const char *label, uint64_t value = 0);
 void TraceDump();
 

@@ -976,7 +976,7 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
     PinnedBuf &hs = I.h_tasks[buf];
     hs.Reserve(task_bytes(n, q_first, q_end));
     ntasks = BuildTasks(swar, cand_begin, n, q_first, q_end, counts, offsets, per_block, hs.as<kern::ScoreTask>(),
-                        &kind);
+                        &kind, guard == 0);
     TraceMark("tasks", ntasks);
     if (const char *dump = getenv("GHOSTM_DEBUG_TASKS")) {  // diagnostics: the launch's tasks and counts
       if (FILE *f = fopen(dump, "ab")) {
@@ -1116,7 +1116,7 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
     int nkind = kScoreRows;
     hs.Reserve(task_bytes(next->n, next->q_first, next->q_end));
     const size_t nt = BuildTasks(swar, next->cand_begin, next->n, next->q_first, next->q_end, counts, offsets,
-                                 per_block, hs.as<kern::ScoreTask>(), &nkind);
+                                 per_block, hs.as<kern::ScoreTask>(), &nkind, guard == 0);
     const size_t nbytes = nt * (nkind == kScorePairs ? 4 : sizeof(kern::ScoreTask));
     I.task_buf[nb].Reserve(nbytes);
     HIP_CHECK(hipMemcpyAsync(I.task_buf[nb].p, hs.p, nbytes, hipMemcpyHostToDevice, S(copy_stream_)));

@@ -302,10 +302,11 @@ constexpr uint64_t kScorePairMax = 16;
 // Below kScorePairMax candidates per query (and with integer patterns) the
 // segment runs k_score_pair over BuildScorePairs' list instead, written into
 // `out` as uint32 entries. `out` has room for ScoreTaskBound(...) tasks and n
-// uint32 entries.
+// uint32 entries. pairs_ok = false (a launch with the re-score guard, which
+// only k_score16f implements) keeps the profile kernels.
 inline size_t BuildTasks(bool swar, uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32_t q_end,
                          const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets,
-                         uint32_t per_block, kern::ScoreTask *out, int *kind_out) {
+                         uint32_t per_block, kern::ScoreTask *out, int *kind_out, bool pairs_ok = true) {
   const char *k2 = getenv("GHOSTM_K2");
   const char *how = getenv("GHOSTM_K2_TASKS");
   const bool force_unit = k2 && strcmp(k2, "unit") == 0, force_rows = k2 && strcmp(k2, "swar16") == 0;
@@ -314,7 +315,8 @@ inline size_t BuildTasks(bool swar, uint64_t cand_begin, uint64_t n, uint32_t q_
   const uint64_t per_query = n / std::max<uint32_t>(1, q_end - q_first);
   uint64_t pair_max = kScorePairMax;
   if (const char *e = getenv("GHOSTM_K2_PAIR_MAX")) pair_max = strtoull(e, nullptr, 10);
-  if (swar && q_end > q_first && !force_unit && !force_rows && !how && (force_pair || per_query < pair_max)) {
+  if (swar && pairs_ok && q_end > q_first && !force_unit && !force_rows && !how &&
+      (force_pair || per_query < pair_max)) {
     *kind_out = kScorePairs;
     return BuildScorePairs(cand_begin, n, q_first, q_end, counts, offsets, reinterpret_cast<uint32_t *>(out));
   }
