@@ -8,6 +8,8 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r5f
 mkdir -p $O
 cd $R
+timeout -k 10 700 python -u -m pytest tests -m gpu -q --maxfail 10 --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { echo "tests failed"; tail -40 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
 summ() {
 python3 - "$1" "$2" <<'PY'
 import json, sys
