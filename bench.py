@@ -539,7 +539,16 @@ def main() -> None:
         framed = half and per.get("score_launches_framed", 0) == per["score_launches"]
         swar = framed and per.get("score_launches_swar", 0) == per["score_launches"]
         unit = swar and per.get("score_launches_unit", 0) == per["score_launches"]
-        if unit:
+        n_pair = per.get("score_launches_pair", 0)
+        pair = swar and n_pair == per["score_launches"]
+        if pair:
+            kname = ("k_score_pair<32> (K2 Gotoh DP over a query-independent pair table: one LDS word per "
+                     "(query residue, two subject residues), 16-bit integer patterns, two candidates per lane; "
+                     "sparse segments)")
+        elif swar and n_pair:
+            kname = (f"k_score_pair<32> on {n_pair:g} of {per['score_launches']:g} launches per step, "
+                     "k_score16f<32,swar> on the rest (K2 Gotoh DP over 16-bit integer patterns)")
+        elif unit:
             kname = ("k_score16f<32,swar,unit> (K2 Gotoh DP, per-column frame over 16-bit integer patterns, "
                      "two candidates per lane; unit-pair profile words: the diagonal sum is one op_sel "
                      "v_pk_mad_u16)")
@@ -576,6 +585,8 @@ def main() -> None:
             "gcups": score_cells / score_t / 1e9 if score_t > 0 else 0.0,
             "avg_launch_ms": score_t * 1e3,
             "guard_rescores_per_step": per.get("score_rechecks", 0),
+            "launches_per_step": {"pair": n_pair, "unit": per.get("score_launches_unit", 0),
+                                  "total": per["score_launches"]},
         }
         if issue and pmc_ok and pmc.get("k_score_valu_insts_per_launch"):
             rate = pmc["k_score_valu_insts_per_launch"] / score_t

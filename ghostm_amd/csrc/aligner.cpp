@@ -884,6 +884,11 @@ void Session::DevicePass(QueryData &q, DbData &d, const std::vector<uint32_t> &c
   uint64_t kTailCands = std::min<uint64_t>(1ull << 20, std::max<uint64_t>(1ull << 17, (c_hi - c_lo) / 4));
   if (const char *e = getenv("GHOSTM_SEGMENT_CANDS")) kSegmentCands = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
   if (const char *e = getenv("GHOSTM_TAIL_CANDS")) kTailCands = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
+  // the first segment's K2 tasks are built while the GPU waits (the later
+  // ones during the previous K2): a head of at most kHeadCands shortens that
+  // wait (GHOSTM_HEAD_CANDS; 0 = no head cap)
+  uint64_t kHeadCands = kTailCands;
+  if (const char *e = getenv("GHOSTM_HEAD_CANDS")) kHeadCands = strtoull(e, nullptr, 10);
   const uint32_t ng = (uint32_t)q.group_first.size();
   // a group's first candidate of this batch (groups outside it have none)
   auto group_begin = [&](uint32_t g) { return std::min(std::max(offsets[q.group_first[g]], c_lo), c_hi); };
@@ -908,8 +913,9 @@ void Session::DevicePass(QueryData &q, DbData &d, const std::vector<uint32_t> &c
     // the text formatting of the one before it (~1.4 ms per 1 M), so little of
     // the formatting is left when the GPU finishes
     // (a carried pass formats nothing: full segments only)
-    const uint64_t target = rem > 2 * kSegmentCands || !final_pass ? kSegmentCands
-                                                                    : std::max<uint64_t>(kTailCands, rem * 3 / 5);
+    uint64_t target = rem > 2 * kSegmentCands || !final_pass ? kSegmentCands
+                                                              : std::max<uint64_t>(kTailCands, rem * 3 / 5);
+    if (g0 == gb0 && kHeadCands && rem > 2 * kHeadCands) target = std::min(target, kHeadCands);
     uint32_t g1 = g0 + 1;
     while (g1 < gb1 && group_begin(g1) - group_begin(g0) < target) ++g1;
     cuts.emplace_back(g0, g1);
@@ -1033,6 +1039,10 @@ void Session::RunQueryChunk(QueryData &q) {
   }
   const uint32_t cap = std::max<uint32_t>(opt_.best, 1);
   dev.ResetCarry(q.dev, cap);
+  if (TraceOn()) {  // timeline only: the carry reset's own time
+    dev.Synchronize();
+    TraceMark("carry_idle");
+  }
   bool carry = false, formatted = false;
   for (size_t di = 0; di < dbs_.size(); ++di) {
     DbData &d = dbs_[di];
@@ -1438,6 +1448,10 @@ void Session::Run(bool stream_to_file) {
   records_on_device_ = true;
   const double t0 = NowSeconds();
   TraceMark("run");
+  if (TraceOn()) {  // timeline only: anything still queued from before the run?
+    dev.Synchronize();
+    TraceMark("run_idle");
+  }
   for (QueryData &q : queries_) {
     RunQueryChunk(q);
     stats_.queries += q.chunk.nseq;
