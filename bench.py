@@ -58,6 +58,7 @@ VALU_ISSUE = os.path.join(REPO, "profiles", "r2_valu_issue.json")
 PMC = os.path.join(REPO, "profiles", "pmc_traffic.json")  # cfg4; other presets: pmc_traffic_<preset>.json
 ISA_MIX = os.path.join(REPO, "profiles", "r3_k2_isa_mix.json")  # k_score16f<32, true> (16-bit profile rows)
 ISA_MIX_UNIT = os.path.join(REPO, "profiles", "r3u_k2_isa_mix.json")  # k_score16f<32, true, true> (unit-pair words)
+ISA_MIX_PAIR = os.path.join(REPO, "profiles", "r5_k2_pair_isa_mix.json")  # k_score_pair<32> (pair table)
 VOP2_IN_MIX_CYCLES = 3.44  # fast VOP2 add inside a 1:2 pk_max3:add stream (profiles/r2c_valu_issue_pmc.txt)
 
 
@@ -468,7 +469,7 @@ def main() -> None:
     # ms, profiles/r4n_e2e/)
     e2e = None
     if not args.no_e2e:
-        runs, files_ok = [], []
+        runs, files_ok, create_s = [], [], []
         for _ in range(5):
             # a fresh output path per run (truncating the last run's 0.5 GB file
             # would free its page-cache pages inside the timed region)
@@ -485,6 +486,7 @@ def main() -> None:
                 dist.barrier()
             te = time.perf_counter()
             with guarded(open_session, "end-to-end session create") as s2:
+                create_s.append(time.perf_counter() - te)
                 if world == 1:
                     s2.run(to_file=True)  # the output file is written while the search runs
                 else:
@@ -509,6 +511,7 @@ def main() -> None:
         dt, e2e_res = sorted(runs)[len(runs) // 2]
         e2e = {"seconds": dt, "value": e2e_res / dt, "unit": "query residues/s", "runs_s": [r[0] for r in runs],
                "statistic": f"median of {len(runs)}",
+               "create_s": create_s,  # this rank's session create per run (file loads, H2D)
                "includes": "session create (query/DB/index file loads from a warm page cache, dirty pages written "
                            "back first; H2D; N > 1: rank-local reads and the "
                            "batch-plan all-gather), the search, text formatting and the output file write "
@@ -599,7 +602,9 @@ def main() -> None:
             # VOP2 2.27 alone and 3.44 at best inside VOP3P streams (the 1:2 mix
             # row). The ceiling takes the cheapest cost of each class, so the
             # kernel's PMC cycles per instruction cannot beat it.
-            mix = (_json(ISA_MIX_UNIT if unit else ISA_MIX) or {}).get("column_bodies")
+            mix = (_json(ISA_MIX_PAIR if pair else ISA_MIX_UNIT if unit else ISA_MIX) or {}).get("column_bodies")
+            if swar and n_pair and not pair:
+                mix = None  # mixed kinds: no single instruction mix
             cyc = pmc.get("k_score_valu_cycles_per_inst")
             c3 = issue.get("cycles_per_inst", {}).get("vop3_class_median")
             if mix and cyc and c3:

@@ -1039,10 +1039,8 @@ void Session::RunQueryChunk(QueryData &q) {
   }
   const uint32_t cap = std::max<uint32_t>(opt_.best, 1);
   dev.ResetCarry(q.dev, cap);
-  if (TraceOn()) {  // timeline only: the carry reset's own time
-    dev.Synchronize();
-    TraceMark("carry_idle");
-  }
+  if (run_sync_) dev.Synchronize();  // (see Run)
+  TraceMark("carry_idle");
   bool carry = false, formatted = false;
   for (size_t di = 0; di < dbs_.size(); ++di) {
     DbData &d = dbs_[di];
@@ -1448,10 +1446,14 @@ void Session::Run(bool stream_to_file) {
   records_on_device_ = true;
   const double t0 = NowSeconds();
   TraceMark("run");
-  if (TraceOn()) {  // timeline only: anything still queued from before the run?
-    dev.Synchronize();
-    TraceMark("run_idle");
-  }
+  // Both streams drained at the start of a run and after each chunk's carry
+  // reset: without these waits (which find the streams idle, < 0.03 ms) a
+  // session's second run waited 10-28 ms before its first K1 kernel
+  // (profiles/r5i/). GHOSTM_RUN_SYNC=0 leaves them out (A/B).
+  const char *rs = getenv("GHOSTM_RUN_SYNC");
+  run_sync_ = !(rs && strcmp(rs, "0") == 0);
+  if (run_sync_) dev.Synchronize();
+  TraceMark("run_idle");
   for (QueryData &q : queries_) {
     RunQueryChunk(q);
     stats_.queries += q.chunk.nseq;

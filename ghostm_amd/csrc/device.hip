@@ -45,22 +45,82 @@ struct PinnedBuf {
   template <class T> T *as() const { return static_cast<T *>(p); }
 };
 
+// Device blocks released by a buffer stay cached for the next one (a session's
+// query/DB/index buffers are released at its end and the next session's create
+// asks for the same sizes: hipMalloc/hipFree cost ~1.5 ms of a cfg3 create,
+// profiles/r5f/cfg3_e2e_trace.log). A block is cached after a device
+// synchronisation, as hipFree would do; a request takes the smallest cached block
+// of 1-2x its size. At most GHOSTM_DEV_POOL_MB (default 8192) stay cached; 0
+// turns the cache off.
+class DevPool {
+ public:
+  static DevPool &Get() {
+    static DevPool pool;
+    return pool;
+  }
+  void *Take(size_t *bytes) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lock(mu_);
+    size_t best = blocks_.size();
+    for (size_t k = 0; k < blocks_.size(); ++k)
+      if (blocks_[k].dev == dev && blocks_[k].bytes >= *bytes && blocks_[k].bytes <= 2 * *bytes &&
+          (best == blocks_.size() || blocks_[k].bytes < blocks_[best].bytes))
+        best = k;
+    if (best == blocks_.size()) return nullptr;
+    void *p = blocks_[best].p;
+    *bytes = blocks_[best].bytes;
+    cached_ -= *bytes;
+    blocks_.erase(blocks_.begin() + (long)best);
+    return p;
+  }
+  void Give(void *p, size_t bytes) {
+    if (!p) return;
+    (void)hipDeviceSynchronize();  // no queued work may still use the block
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lock(mu_);
+    if (cached_ + bytes > cap_) {
+      (void)hipFree(p);
+      return;
+    }
+    blocks_.push_back(Block{p, bytes, dev});
+    cached_ += bytes;
+  }
+
+ private:
+  DevPool() {
+    const char *e = getenv("GHOSTM_DEV_POOL_MB");
+    cap_ = (size_t)(e ? strtoull(e, nullptr, 10) : 8192ull) << 20;
+  }
+  struct Block {
+    void *p;
+    size_t bytes;
+    int dev;
+  };
+  std::mutex mu_;
+  std::vector<Block> blocks_;
+  size_t cached_ = 0, cap_ = 0;
+};
+
 struct DevBuf {
   void *p = nullptr;
   size_t bytes = 0;
   void Reserve(size_t b) {
     if (b <= bytes) return;
-    if (p) HIP_CHECK(hipFree(p));
-    p = nullptr;
-    bytes = 0;
+    Release();
     size_t want = std::max<size_t>(b, 256);
-    if (TraceOn()) TraceMark("dev_alloc", want);
-    HIP_CHECK(hipMalloc(&p, want));
+    if ((p = DevPool::Get().Take(&want))) {
+      if (TraceOn()) TraceMark("dev_reuse", want);
+    } else {
+      if (TraceOn()) TraceMark("dev_alloc", want);
+      HIP_CHECK(hipMalloc(&p, want));
+    }
     bytes = want;
   }
   void Release() {
     if (p && TraceOn()) TraceMark("dev_free", bytes);
-    if (p) (void)hipFree(p);
+    DevPool::Get().Give(p, bytes);
     p = nullptr;
     bytes = 0;
   }
@@ -91,6 +151,7 @@ Layout ChooseLayout(uint32_t L, uint32_t width) {
 }
 
 thread_local std::string g_last_error;
+
 
 }  // namespace
 
@@ -1050,12 +1111,23 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
   HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
   const dim3 grid((uint32_t)ntasks), block(kern::kScoreBlock);
   if (pairs) {
-    // persistent: one 768-thread workgroup per CU (the pair table), looping over the pairs
-    const uint32_t per_wg = (kern::kPairBlock / 64) * lay.gpw;
+    // persistent: one 768-thread workgroup per CU (the 96 KB pair table), looping
+    // over the pairs. At most 16 rows per lane: with 32 (the profile kernels'
+    // layout at L > 64) K2 took 3.57 against 3.40 ms per cfg2 step, same box
+    // (profiles/r5k/); GHOSTM_K2_PAIR_S=8|16|32 forces the rows per lane (A/B).
+    // The kernel is bound by the table's LDS bank conflicts: two workgroups per CU
+    // (a 78.7 KB table) or 1024-thread workgroups measured slower (profiles/r5i, r5j).
+    uint32_t ps = std::min<uint32_t>((uint32_t)lay.S, 16);
+    if (const char *e = getenv("GHOSTM_K2_PAIR_S")) ps = (uint32_t)atoi(e);
+    const uint32_t pg = ps == 8 || ps == 16 || ps == 32 ? lay.Lpad / ps : 0;
+    const Layout play = pg >= 1 && pg <= 16 && pg * ps == lay.Lpad ? Layout{(int)ps, pg, lay.Lpad, 64 / pg} : lay;
+    a.G = play.G;
+    a.gpw = play.gpw;
+    const uint32_t per_wg = (kern::kPairBlock / 64) * play.gpw;
     const dim3 pgrid(std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)I.cus, (uint32_t)((ntasks + per_wg - 1) / per_wg))));
     const dim3 pblock(kern::kPairBlock);
     const size_t plds = (size_t)kern::kPairK2Words * 4;
-    switch (lay.S) {
+    switch (play.S) {
       case 32: hipLaunchKernelGGL((kern::k_score_pair<32>), pgrid, pblock, plds, S(stream_), a); break;
       case 16: hipLaunchKernelGGL((kern::k_score_pair<16>), pgrid, pblock, plds, S(stream_), a); break;
       default: hipLaunchKernelGGL((kern::k_score_pair<8>), pgrid, pblock, plds, S(stream_), a); break;
@@ -1269,11 +1341,22 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
     hipLaunchKernelGGL(kern::k_csort_scatter, gsort, b256, 0, S(stream_), I.tb_key.as<uint32_t>(), n, true,
                        hist1, cur1, I.tb_order1.as<uint32_t>());
     kern::TbScanArgs sa{};
+    // the scan's rows per lane: GHOSTM_K3_SCAN_S=16 halves them (twice the lanes
+    // per hit; its strips map onto the key DP's by a shift)
+    Layout slay = lay;
+    if (const char *e = getenv("GHOSTM_K3_SCAN_S")) {
+      const uint32_t ss = (uint32_t)atoi(e);
+      const uint32_t sg = ss == 8 || ss == 16 || ss == 32 ? lay.Lpad / ss : 0;
+      if (sg >= lay.G && sg <= 16 && sg * ss == lay.Lpad) slay = Layout{(int)ss, sg, lay.Lpad, 64 / sg};
+    }
+    uint32_t shift = 0;
+    while ((lay.G << shift) < slay.G) ++shift;
+    sa.strip_shift = shift;
     sa.qseq = a.qseq;
     sa.L = a.L;
-    sa.Lpad = lay.Lpad;
-    sa.G = lay.G;
-    sa.gpw = lay.gpw;
+    sa.Lpad = slay.Lpad;
+    sa.G = slay.G;
+    sa.gpw = slay.gpw;
     sa.db = a.db;
     sa.mat = I.mat_raw.as<int>();
     sa.qid = a.qid;
@@ -1301,7 +1384,7 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
     sa.hist = hist2;
     sa.cells = a.cells ? a.cells + 1 : nullptr;
     // every CU one workgroup (kScanBlock threads), looping over the sorted pairs
-    const uint32_t pairs_per_block = (kern::kScanBlock / 64) * lay.gpw;
+    const uint32_t pairs_per_block = (kern::kScanBlock / 64) * slay.gpw;
     const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)I.cus,
                                                                      (n + pairs_per_block - 1) / pairs_per_block));
     // exact windows (cut at the subject's start) need the DB's subject table
@@ -1332,7 +1415,7 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
   else if (half) GHOSTM_SCAN1(SS, true, false, false);           \
   else if (exact) GHOSTM_SCAN1(SS, false, true, false);          \
   else GHOSTM_SCAN1(SS, false, false, false);
-    switch (lay.S) {
+    switch (slay.S) {
       case 32: GHOSTM_SCAN(32); break;
       case 16: GHOSTM_SCAN(16); break;
       default: GHOSTM_SCAN(8); break;

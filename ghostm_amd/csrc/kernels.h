@@ -2090,6 +2090,9 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
 constexpr uint32_t kPairK2Codes = 27;  // DB codes 0..25 and kFillCode (26)
 constexpr uint32_t kPairK2Stride = 33;  // dwords per (a, b) code pair: odd, as K3a's kPairStride
 constexpr uint32_t kPairK2Words = kPairK2Codes * kPairK2Codes * kPairK2Stride;
+// query row codes in the table: residues 0..24, kPairPadCode for the padding
+// rows (k_fwd_codes)
+constexpr uint32_t kPairPadCode = 25;
 constexpr int kPairBlock = 768;
 constexpr uint32_t kPairSingle = kPairSingleBit;  // pair entry: no second candidate
 
@@ -2105,7 +2108,7 @@ __global__ void k_fwd_codes(const uint8_t *qseq, uint32_t nq, uint32_t L, uint32
   uint32_t word = 0;
   for (uint32_t v = 0; v < 4; ++v) {
     const uint32_t r = 4 * w + v;
-    word |= (r >= pad ? (uint32_t)qseq[q * L + (r - pad)] * 4 : kPadCode * 4) << (8 * v);
+    word |= (r >= pad ? (uint32_t)qseq[q * L + (r - pad)] * 4 : kPairPadCode * 4) << (8 * v);
   }
   out[t] = word;
 }
@@ -2120,13 +2123,13 @@ __global__ __launch_bounds__(kPairBlock) void k_score_pair(ScoreArgs a) {
     const uint32_t drop = (uint32_t)(0x10000u - (a.swar_low - 64u)) & 0xFFFFu;
     auto enc = [&](uint32_t q, uint32_t c) -> uint32_t {  // BuildProfile16<C, true, true>'s value
       if (c == kSeqEnd) return a.swar_restart;
-      if (q == kPadCode || c > kSeqEnd) return drop;
+      if (q >= kPairPadCode || c > kSeqEnd) return drop;
       return (uint32_t)(a.mat[c * 32 + q] + extp) & 0xFFFFu;
     };
     for (uint32_t e = threadIdx.x; e < kPairK2Words; e += kPairBlock) {
       const uint32_t pr = e / kPairK2Stride, q = e - pr * kPairK2Stride;
       const uint32_t ca = pr / kPairK2Codes, cb = pr - ca * kPairK2Codes;
-      s_pk2[e] = q < 32 ? enc(q, ca) | enc(q, cb) << 16 : 0u;
+      s_pk2[e] = q <= kPairPadCode ? enc(q, ca) | enc(q, cb) << 16 : 0u;
     }
   }
   __syncthreads();
@@ -3356,6 +3359,7 @@ struct TbScanArgs {
   // runs the lanes of strips 0..i* only (kTbStripClasses); else min(j* + 1, kSortBins - 1)
   uint32_t *skey;
   uint32_t strips;
+  uint32_t strip_shift;        // the key DP's strip = the scan's strip >> strip_shift (scan G = key G << shift)
 };
 
 // The scan keeps each row's table offset in its own register: a VOP2 address
@@ -3695,7 +3699,7 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
     }
     auto skey = [&](int c, uint32_t strip, int b) -> uint32_t {
       if (!a.strips) return min((uint32_t)c + 1, kSortBins - 1);
-      return (b > 0 ? strip : 0u) * kStripBins + min((uint32_t)c + 1, kStripBins - 1);
+      return (b > 0 ? strip >> a.strip_shift : 0u) * kStripBins + min((uint32_t)c + 1, kStripBins - 1);
     };
     if (i == 0 && wA) {
       a.ncols[sA] = (uint32_t)CA + 1;

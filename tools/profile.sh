@@ -36,3 +36,4 @@ timeout -k 10 400 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_A
 echo "lds done"
 NQ=$(python3 -c "import sys; sys.path.insert(0, '$R'); from ghostm_amd.workloads import WORKLOADS; print(WORKLOADS['$PRESET']['queries'])")
 python3 "$R/tools/pmc_summary.py" --round "$ROUND" --prof "$OUT" --queries "$NQ" --preset "$PRESET"
+cp "$R/profiles/${ROUND}_pmc.json" "$R/profiles/pmc_traffic_${PRESET}.json" "$OUT/" 2>/dev/null || true
