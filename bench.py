@@ -366,13 +366,6 @@ def main() -> None:
 
     for _ in range(args.warmup):
         step()
-    # The run after a session's first one starts with a one-time 10-28 ms stall
-    # of the GPU queue (before its first kernel; device and pinned allocations
-    # traced: none in that run) unless ~0.2 s pass after the first run
-    # (DESIGN.md §7). The warmup absorbs first-run effects; this settle keeps
-    # that one out of the timed steps. GHOSTM_BENCH_WARM_SETTLE_S=0 disables it.
-    if args.warmup:
-        time.sleep(float(os.environ.get("GHOSTM_BENCH_WARM_SETTLE_S", "0.25")))
 
     def sync():
         if dist is not None:
