@@ -608,6 +608,11 @@ void Session::Load(uint32_t shard_rank, uint32_t shard_world, bool local, std::v
       std::memcpy(static_cast<char *>(dst) + lo, static_cast<const char *>(src) + lo, hi - lo);
     });
   });
+  dev.SetHostParallel([copiers](size_t parts, const std::function<void(size_t)> &fn) {
+    ParallelFor(parts, copiers, [&](size_t b, size_t e, unsigned) {
+      for (size_t k = b; k < e; ++k) fn(k);
+    });
+  });
   dev.SetMatrix(opt_.matrix.m.data());
 
   // query chunks: -S start (or 0) .. -L end, as Execute walks them
@@ -1026,8 +1031,11 @@ void Session::RunQueryChunk(QueryData &q) {
   sc.threshold = opt_.threshold;
   sc.shift = opt_.shift;
   sc.log_region = opt_.log_region;
-  std::vector<uint32_t> counts;
-  std::vector<uint64_t> offsets;
+  // K1's per-query counts and offsets: session buffers, reused by every chunk
+  // and run (a fresh vector's zero-fill and first-touch faults sat before K1's
+  // first kernel: 6 MB per cfg4 chunk)
+  std::vector<uint32_t> &counts = seed_counts_;
+  std::vector<uint64_t> &offsets = seed_offsets_;
   // the device merge needs every DB chunk's subject table; GHOSTM_MERGE=host
   // keeps the host merge (tests)
   bool device_merge = true;

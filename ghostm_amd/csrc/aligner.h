@@ -226,6 +226,8 @@ class Session {
   std::unique_ptr<TaskQueue> writer_;  // streamed output (Run(true)), in part order
   int stream_fd_ = -1;
   bool run_sync_ = true;  // drain the streams at run and chunk starts (Run)
+  std::vector<uint32_t> seed_counts_;  // K1 counts/offsets of the current chunk (RunQueryChunk)
+  std::vector<uint64_t> seed_offsets_;
   uint64_t stream_off_ = 0;
   bool stream_failed_ = false, streamed_ = false;
   std::unique_ptr<LineFormat> format_;

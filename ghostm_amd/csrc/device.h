@@ -104,6 +104,10 @@ class DeviceModule {
   // Copies n bytes host to host (the session sets a parallel one; default memcpy).
   using HostCopyFn = std::function<void(void *dst, const void *src, size_t n)>;
   void SetHostCopy(HostCopyFn fn);
+  // Runs fn(k), k < parts, on host worker threads (the session sets its pool;
+  // used by the K2 pair-list build and K1's count pass).
+  using HostParallelFn = std::function<void(size_t parts, const std::function<void(size_t)> &fn)>;
+  void SetHostParallel(HostParallelFn fn);
   // Host to device through page-locked staging on the main stream (see device.hip).
   void StagedUpload(void *dst, const void *src, size_t bytes);
   DevQuery *UploadQuery(const uint8_t *seq, uint32_t nseq, uint32_t L);
@@ -208,6 +212,7 @@ class DeviceModule {
   int device_ = -1;
   void *stream_ = nullptr;
   HostCopyFn host_copy_;
+  HostParallelFn host_par_;
   void *copy_stream_ = nullptr;  // D2H of selections and K2 task uploads, beside the kernels
   DeviceTimes times_;
   uint64_t records_ = 0;

@@ -245,7 +245,7 @@ struct DeviceModule::Impl {
   hipEvent_t ev_done = nullptr, ev_tasks = nullptr; // end of a segment's selection; next tasks uploaded
   // K1 read-backs (per-query bin and candidate counts) land in page-locked
   // staging: GHOSTM_K1_PINNED=0 keeps the pageable copies (A/B)
-  PinnedBuf h_nbins, h_counts, h_qlist;
+  PinnedBuf h_nbins, h_counts, h_qlist, h_offsets;
   DevBuf counters;     // K2: u64 [0] score cells, u32 at [2] guard count
   DevBuf tb_counters;  // K3: u64 [0] traceback cells, [1] K3a scan cells, [2] hits traced (k_finalize)
   bool matrix_set = false;
@@ -450,6 +450,7 @@ void DeviceModule::SetMatrix(const int *m) {
 }
 
 void DeviceModule::SetHostCopy(HostCopyFn fn) { host_copy_ = std::move(fn); }
+void DeviceModule::SetHostParallel(HostParallelFn fn) { host_par_ = std::move(fn); }
 
 // Host bytes to the device through page-locked staging: pieces of kStagePiece
 // bytes, each copied into a ring slot by the host copy function (the session's
@@ -676,12 +677,17 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
   Use();
   Impl &I = *impl_;
   const uint32_t nq = q->nseq;
-  counts->assign(nq, 0);
-  offsets->assign(nq, 0);
+  // every element is written below (counts by the count pass or the read-back,
+  // offsets by the offset pass): a reused vector is not cleared first
+  counts->resize(nq);
+  offsets->resize(nq);
   I.ncand = 0;
-  if (nq == 0) return 0;
   const uint32_t seed_len = SeedLength(cfg.seed_mask);
-  if (seed_len == 0 || seed_len > q->L) return 0;
+  if (nq == 0 || seed_len == 0 || seed_len > q->L) {
+    std::fill(counts->begin(), counts->end(), 0u);
+    std::fill(offsets->begin(), offsets->end(), 0ull);
+    return 0;
+  }
   if (cfg.shift == 0) throw Error("shift size must be positive");
   const uint32_t nlists = (q->L - seed_len) / cfg.shift + 1;
   if (nlists > kern::kMaxLists) throw Error("too many seed lists");
@@ -846,9 +852,40 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
   }
   TraceMark("k1b_enq");
   HIP_CHECK(hipStreamSynchronize(S(stream_)));
-  if (pinned) std::memcpy(counts->data(), I.h_counts.p, (size_t)nq * 4);
   TraceMark("k1b_done");
-  if (filter) {
+  // counts into the host vector, offsets into it and into page-locked staging
+  // (uploaded by DMA), in parts on the worker threads: the GPU waits for this
+  // pass (cfg4: 505 K queries per chunk)
+  I.h_offsets.Reserve((size_t)nq * 8);
+  unsigned long long *h_off = I.h_offsets.as<unsigned long long>();
+  const size_t parts = nq >= 65536 && host_par_ ? 16 : 1;
+  auto part_lo = [&](size_t k) { return (uint32_t)((uint64_t)nq * k / parts); };
+  auto for_parts = [&](const std::function<void(size_t)> &fn) {
+    if (parts > 1) host_par_(parts, fn);
+    else fn(0);
+  };
+  std::vector<uint64_t> part_sum(parts + 1, 0);
+  std::vector<uint8_t> part_over(parts, 0);
+  std::vector<std::vector<uint32_t>> part_wide(parts);
+  auto count_pass = [&](const uint32_t *src) {
+    for_parts([&](size_t k) {
+      uint64_t s = 0;
+      bool over = false;
+      uint32_t *dst = counts->data();
+      for (uint32_t i = part_lo(k); i < part_lo(k + 1); ++i) {
+        const uint32_t c = src[i];
+        if (src != dst) dst[i] = c;
+        s += c;
+        over |= c == kern::kOverflow;
+      }
+      part_sum[k + 1] = s;
+      part_over[k] = over;
+    });
+  };
+  count_pass(pinned ? I.h_counts.as<uint32_t>() : counts->data());
+  bool overflow = false;
+  for (uint8_t o : part_over) overflow |= o != 0;
+  if (filter && overflow) {
     // queries whose filtered queue overflowed: the unfiltered table redoes them
     std::vector<uint32_t> redo[3];
     for (int c = 0; c < 3; ++c)
@@ -870,31 +907,36 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
       HIP_CHECK(hipMemcpyAsync(counts->data(), I.counts.p, (size_t)nq * 4, hipMemcpyDeviceToHost, S(stream_)));
       HIP_CHECK(hipStreamSynchronize(S(stream_)));
       times_.seed_filter_overflows += all.size();
+      count_pass(counts->data());
     }
   }
-
-  uint64_t total = 0;
+  for (size_t k = 0; k < parts; ++k) part_sum[k + 1] += part_sum[k];
+  const uint64_t total = part_sum[parts];
+  for_parts([&](size_t k) {
+    uint64_t o = part_sum[k];
+    const uint32_t *cnt = counts->data();
+    uint64_t *off = offsets->data();
+    for (uint32_t i = part_lo(k); i < part_lo(k + 1); ++i) {
+      off[i] = o;
+      h_off[i] = o;
+      if (cnt[i] > slot_cap) part_wide[k].push_back(i);
+      o += cnt[i];
+    }
+  });
+  // queries with more candidates than a slot, by size class in query order
   std::vector<uint32_t> wide[4];
   std::vector<unsigned long long> &wide_goff = I.h_wide_goff;  // outlive the async copies below
   wide_goff.clear();
-  for (uint32_t i = 0; i < nq; ++i) {
-    (*offsets)[i] = total;
-    total += (*counts)[i];
-  }
-  for (int c = 0; c < 4; ++c) {
-    size_t gi = 0;
-    for (uint32_t qi : cls[c]) {
-      if ((*counts)[qi] > slot_cap) {
-        wide[c].push_back(qi);
-        if (c == 3) wide_goff.push_back(goff[gi]);
-      }
-      ++gi;
+  for (const std::vector<uint32_t> &pw : part_wide)
+    for (uint32_t qi : pw) {
+      const int c = class_of(nbins[qi]);
+      wide[c].push_back(qi);
+      if (c == 3) wide_goff.push_back(goff[(size_t)(std::lower_bound(cls[3].begin(), cls[3].end(), qi) - cls[3].begin())]);
     }
-  }
   I.ncand = total;
   I.cand_start.Reserve(total * 4 + 4);
   I.cand_qid.Reserve(total * 4 + 4);
-  HIP_CHECK(hipMemcpyAsync(I.offsets.p, offsets->data(), (size_t)nq * 8, hipMemcpyHostToDevice, S(stream_)));
+  HIP_CHECK(hipMemcpyAsync(I.offsets.p, h_off, (size_t)nq * 8, hipMemcpyHostToDevice, S(stream_)));
   // slot -> compact
   hipLaunchKernelGGL(kern::k_compact, dim3((nq + 3) / 4), dim3(256), 0, S(stream_),
                      I.slots.as<uint32_t>(), slot_cap, I.counts.as<uint32_t>(), (const uint8_t *)nullptr,
@@ -1037,7 +1079,7 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
     PinnedBuf &hs = I.h_tasks[buf];
     hs.Reserve(task_bytes(n, q_first, q_end));
     ntasks = BuildTasks(swar, cand_begin, n, q_first, q_end, counts, offsets, per_block, hs.as<kern::ScoreTask>(),
-                        &kind, guard == 0);
+                        &kind, guard == 0, &host_par_);
     TraceMark("tasks", ntasks);
     if (const char *dump = getenv("GHOSTM_DEBUG_TASKS")) {  // diagnostics: the launch's tasks and counts
       if (FILE *f = fopen(dump, "ab")) {

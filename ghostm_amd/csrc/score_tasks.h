@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <utility>
 #include <vector>
 
@@ -15,6 +16,10 @@
 
 
 namespace ghostm {
+
+// Runs fn(k) for k in [0, parts) on host worker threads and returns when all are
+// done (the session's ParallelFor; null = one thread).
+using HostParallelFn = std::function<void(size_t parts, const std::function<void(size_t)> &fn)>;
 
 // K2 tasks: runs of <= per_block consecutive candidates spanning <= Qmax queries,
 // written straight into page-locked staging (no fresh host vector per segment:
@@ -267,18 +272,39 @@ inline void CountTasks(uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32
 // index (from cand_begin) of a pair's first candidate, kPairSingle set when it
 // has no second (a query's odd last one). Returns the number of pairs; `out`
 // has room for n entries.
+// With `par` and many queries the query range is cut into parts: each part's
+// pairs are counted, then written at the part's prefix (the same list).
 inline size_t BuildScorePairs(uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32_t q_end,
                               const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets,
-                              uint32_t *out) {
-  size_t np = 0;
+                              uint32_t *out, const HostParallelFn *par = nullptr) {
   const uint64_t cand_end = cand_begin + n;
-  for (uint32_t qi = q_first; qi < q_end; ++qi) {
-    const uint64_t lo = std::max<uint64_t>(offsets[qi], cand_begin);
-    const uint64_t hi = std::min<uint64_t>(offsets[qi] + counts[qi], cand_end);
-    for (uint64_t c = lo; c < hi; c += 2)
-      out[np++] = (uint32_t)(c - cand_begin) | (c + 1 < hi ? 0u : kern::kPairSingleBit);
-  }
-  return np;
+  auto write = [&](uint32_t qa, uint32_t qb, size_t np) {
+    for (uint32_t qi = qa; qi < qb; ++qi) {
+      const uint64_t lo = std::max<uint64_t>(offsets[qi], cand_begin);
+      const uint64_t hi = std::min<uint64_t>(offsets[qi] + counts[qi], cand_end);
+      for (uint64_t c = lo; c < hi; c += 2)
+        out[np++] = (uint32_t)(c - cand_begin) | (c + 1 < hi ? 0u : kern::kPairSingleBit);
+    }
+    return np;
+  };
+  constexpr uint32_t kPartQueries = 4096;
+  const uint32_t nqr = q_end > q_first ? q_end - q_first : 0;
+  if (!par || !*par || nqr < 2 * kPartQueries) return write(q_first, q_end, 0);
+  const size_t parts = std::min<size_t>(16, nqr / kPartQueries);
+  auto cut = [&](size_t k) { return q_first + (uint32_t)((uint64_t)nqr * k / parts); };
+  std::vector<size_t> at(parts + 1, 0);
+  (*par)(parts, [&](size_t k) {
+    size_t np = 0;
+    for (uint32_t qi = cut(k); qi < cut(k + 1); ++qi) {
+      const uint64_t lo = std::max<uint64_t>(offsets[qi], cand_begin);
+      const uint64_t hi = std::min<uint64_t>(offsets[qi] + counts[qi], cand_end);
+      if (hi > lo) np += (size_t)((hi - lo + 1) / 2);
+    }
+    at[k + 1] = np;
+  });
+  for (size_t k = 0; k < parts; ++k) at[k + 1] += at[k];
+  (*par)(parts, [&](size_t k) { write(cut(k), cut(k + 1), at[k]); });
+  return at[parts];
 }
 
 // Which K2 kernel runs a segment (ScoreKind) and its work list.
@@ -306,7 +332,8 @@ constexpr uint64_t kScorePairMax = 16;
 // only k_score16f implements) keeps the profile kernels.
 inline size_t BuildTasks(bool swar, uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32_t q_end,
                          const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets,
-                         uint32_t per_block, kern::ScoreTask *out, int *kind_out, bool pairs_ok = true) {
+                         uint32_t per_block, kern::ScoreTask *out, int *kind_out, bool pairs_ok = true,
+                         const HostParallelFn *par = nullptr) {
   const char *k2 = getenv("GHOSTM_K2");
   const char *how = getenv("GHOSTM_K2_TASKS");
   const bool force_unit = k2 && strcmp(k2, "unit") == 0, force_rows = k2 && strcmp(k2, "swar16") == 0;
@@ -318,7 +345,7 @@ inline size_t BuildTasks(bool swar, uint64_t cand_begin, uint64_t n, uint32_t q_
   if (swar && pairs_ok && q_end > q_first && !force_unit && !force_rows && !how &&
       (force_pair || per_query < pair_max)) {
     *kind_out = kScorePairs;
-    return BuildScorePairs(cand_begin, n, q_first, q_end, counts, offsets, reinterpret_cast<uint32_t *>(out));
+    return BuildScorePairs(cand_begin, n, q_first, q_end, counts, offsets, reinterpret_cast<uint32_t *>(out), par);
   }
   if (swar && q_end > q_first && !force_rows && !how && !force_unit && per_query >= 96) {
     unit = true;  // dense (cfg 4: 127 per query): runs of two queries fill their blocks, no count needed

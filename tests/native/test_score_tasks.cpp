@@ -7,6 +7,7 @@
 // only on a query's odd last candidate.
 #include <cstdio>
 #include <random>
+#include <thread>
 #include <vector>
 
 #include "../../ghostm_amd/csrc/score_tasks.h"
@@ -160,6 +161,38 @@ int main() {
       if (mode == 0) paired_waves += w;
       if (mode == 1) consec_waves += w;
     }
+  }
+  // the pair list built in parts on threads equals the one-thread list
+  // (BuildScorePairs with a HostParallelFn, many queries)
+  for (int trial = 0; trial < 20; ++trial) {
+    const uint32_t nq = 8192 + (uint32_t)(rng() % 60000);
+    std::vector<uint32_t> counts(nq);
+    std::vector<uint64_t> offsets(nq);
+    std::poisson_distribution<uint32_t> pois(1.0 + (double)(rng() % 20));
+    uint64_t total = 0;
+    for (uint32_t q = 0; q < nq; ++q) {
+      offsets[q] = total;
+      counts[q] = rng() % 5 == 0 ? 0 : pois(rng);
+      total += counts[q];
+    }
+    if (total < 2) continue;
+    const uint64_t b = rng() % (total / 2), e = total - rng() % (total / 4 + 1);
+    uint32_t q0 = 0, q1 = nq;
+    while (q0 < nq && offsets[q0] + counts[q0] <= b) ++q0;
+    while (q1 > 0 && offsets[q1 - 1] >= e) --q1;
+    std::vector<uint32_t> one(e - b + 1), many(e - b + 1);
+    const size_t n1 = ghostm::BuildScorePairs(b, e - b, q0, q1, counts, offsets, one.data());
+    ghostm::HostParallelFn par = [](size_t parts, const std::function<void(size_t)> &fn) {
+      std::vector<std::thread> ts;
+      for (size_t k = parts; k-- > 0;) ts.emplace_back(fn, k);  // parts started in reverse order
+      for (auto &t : ts) t.join();
+    };
+    const size_t n2 = ghostm::BuildScorePairs(b, e - b, q0, q1, counts, offsets, many.data(), &par);
+    if (n1 != n2 || !std::equal(one.begin(), one.begin() + (long)n1, many.begin())) {
+      printf("parallel pair list differs (%zu against %zu pairs, %u queries)\n", n2, n1, q1 - q0);
+      return 1;
+    }
+    ++trials;
   }
   printf("%llu trials ok; waves: paired %llu, consecutive %llu\n", (unsigned long long)trials,
          (unsigned long long)paired_waves, (unsigned long long)consec_waves);

@@ -12,7 +12,7 @@ import subprocess
 def test_score_tasks(tmp_path):
     src = os.path.join(os.path.dirname(__file__), "native", "test_score_tasks.cpp")
     exe = str(tmp_path / "test_score_tasks")
-    subprocess.run(["g++", "-O2", "-std=c++17", src, "-o", exe], check=True)
+    subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", src, "-o", exe], check=True)
     r = subprocess.run([exe], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "trials ok" in r.stdout
