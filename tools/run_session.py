@@ -41,10 +41,11 @@ def main() -> None:
     ap.add_argument("--workdir", default="/tmp/ghostm_run_session")
     ap.add_argument("--kfd", action="store_true")
     ap.add_argument("--out", default=os.devnull, help="output file (-o); bench.py writes a real file")
+    ap.add_argument("--queries", type=int, default=0, help="the first N queries of the preset (0: all)")
     args = ap.parse_args()
     w = workloads.WORKLOADS[args.preset]
     db = workloads.make_db(args.preset, os.path.join(args.workdir, "db"))
-    q = workloads.make_queries(args.preset, os.path.join(args.workdir, "q"), 0, w["queries"])
+    q = workloads.make_queries(args.preset, os.path.join(args.workdir, "q"), 0, args.queries or w["queries"])
     with Session(["-i", q, "-d", db, "-o", args.out, "-D", "0"] + list(w["aln"])) as s:
         if args.kfd:
             print("kfd after create", kfd_counters(), flush=True)
