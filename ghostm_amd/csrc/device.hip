@@ -1510,6 +1510,12 @@ void DeviceModule::ResetCarry(DevQuery *q, uint32_t cap) {
   I.carry_hits.Reserve(ng * cap * sizeof(kern::SlotHit) + 8);
   I.carry_count.Reserve(ng * 4 + 4);
   if (ng) HIP_CHECK(hipMemsetAsync(I.carry_count.p, 0, ng * 4, S(stream_)));
+  // every chunk starts its K2 task buffers at the same one, so a repeated run
+  // gives each segment the buffer pair it had before: with an odd number of
+  // segments the turns alternated between runs, and the second run grew the
+  // other staging buffer (a 35 MB hipHostMalloc, 6.4 ms, in the 125 K-query
+  // shard's second run, profiles/r5u/)
+  if (!I.prepared.valid) I.task_turn = 0;
 }
 
 void DeviceModule::SetChunkBases(const uint32_t *bases, uint32_t n) {
