@@ -85,6 +85,7 @@ struct DeviceTimes {
   uint64_t score_launches_swar = 0;  // ... of the framed kernel over 16-bit integer patterns (k_score16f<S, true>)
   uint64_t score_launches_unit = 0;  // ... of its unit-pair profile variant (k_score16f<S, true, true>)
   uint64_t score_launches_pair = 0;  // sparse segments: the pair-table kernel (k_score_pair)
+  uint64_t seed_compact_redo = 0;    // K1 compactions re-run by the host (overflow, buffer growth)
   uint64_t seed_filter_overflows = 0;             // ... queries redone by k_seed_hash (queue overflow)
   uint64_t traced_hits = 0;                       // device merge: hits selected from new candidates (K3 run)
 };
@@ -150,6 +151,10 @@ class DeviceModule {
                    uint32_t base_search_length, const GapConfig &gap, const ScoreSegment *next);
   bool ScoreGuarded() const;
   void ScoreFinish();
+  // With ScoreDeferNext(true), ScoreLaunch only records `next`; ScorePrepareNext
+  // builds and uploads its tasks (call it after enqueueing the segment's K4/K3).
+  void ScoreDeferNext(bool on) { defer_next_ = on; }
+  void ScorePrepareNext(const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets);
 
   uint32_t ScorePerBlock(DevQuery *q, uint32_t base_search_length, const GapConfig &gap) const;
 
@@ -213,6 +218,7 @@ class DeviceModule {
   void *stream_ = nullptr;
   HostCopyFn host_copy_;
   HostParallelFn host_par_;
+  bool defer_next_ = false;
   void *copy_stream_ = nullptr;  // D2H of selections and K2 task uploads, beside the kernels
   DeviceTimes times_;
   uint64_t records_ = 0;

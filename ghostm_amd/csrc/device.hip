@@ -216,6 +216,13 @@ struct DeviceModule::Impl {
     int S = 32;
     kern::ScoreArgs args{};
   } score_state;
+  struct DeferredNext {  // ScoreLaunch's next segment, built by ScorePrepareNext
+    bool valid = false;
+    DeviceModule::ScoreSegment seg{};
+    bool swar = false, pairs_ok = true;
+    uint32_t per_block = 0;
+    size_t bytes = 0;
+  } deferred;
   // K3 work (tb_sort: two histograms + total, two cursor arrays)
   DevBuf tb_qid, tb_end, tb_start, tb_ml;
   DevBuf tb_width, tb_ncols, tb_skey, tb_key, tb_order1, tb_order2, tb_sort, tb_pair_a, tb_pair_b, tb_best;
@@ -246,6 +253,7 @@ struct DeviceModule::Impl {
   // K1 read-backs (per-query bin and candidate counts) land in page-locked
   // staging: GHOSTM_K1_PINNED=0 keeps the pageable copies (A/B)
   PinnedBuf h_nbins, h_counts, h_qlist, h_offsets;
+  DevBuf offset_parts;                              // K1 device offsets: per-block sums, then prefixes
   DevBuf counters;     // K2: u64 [0] score cells, u32 at [2] guard count
   DevBuf tb_counters;  // K3: u64 [0] traceback cells, [1] K3a scan cells, [2] hits traced (k_finalize)
   bool matrix_set = false;
@@ -844,14 +852,44 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
   }
   times_.seed_launches_hash += hash ? 1 : 0;
   times_.seed_launches_filter += filter ? 1 : 0;
+  if (const char *e = getenv("GHOSTM_K1_FORCE_OVERFLOW"); e && filter && atoi(e) > 0)
+    hipLaunchKernelGGL(kern::k_force_overflow, dim3((nq + 255) / 256), dim3(256), 0, S(stream_),
+                       I.counts.as<uint32_t>(), I.nelem.as<uint32_t>(), nq, (uint32_t)atoi(e), caps[2]);
   if (pinned) {
     I.h_counts.Reserve((size_t)nq * 4);
     HIP_CHECK(hipMemcpyAsync(I.h_counts.p, I.counts.p, (size_t)nq * 4, hipMemcpyDeviceToHost, S(stream_)));
   } else {
     HIP_CHECK(hipMemcpyAsync(counts->data(), I.counts.p, (size_t)nq * 4, hipMemcpyDeviceToHost, S(stream_)));
   }
+  HIP_CHECK(hipEventRecord(I.ev_nb, S(stream_)));
+  // the offsets and the compaction on the device behind the count read-back,
+  // while the host reads the counts (it re-runs the copy only after a queue
+  // overflow or when the candidate buffers had to grow; GHOSTM_K1_DEVOFF=0 keeps
+  // the host offsets, A/B)
+  const char *devoff_env = getenv("GHOSTM_K1_DEVOFF");
+  const bool dev_off = !(devoff_env && strcmp(devoff_env, "0") == 0);
+  const uint64_t cand_cap = std::min(I.cand_start.bytes, I.cand_qid.bytes) / 4;
+  auto launch_compact = [&](uint64_t cap) {
+    hipLaunchKernelGGL(kern::k_compact, dim3((nq + 3) / 4), dim3(256), 0, S(stream_),
+                       I.slots.as<uint32_t>(), slot_cap, I.counts.as<uint32_t>(), (const uint8_t *)nullptr,
+                       I.offsets.as<unsigned long long>(), nq, I.cand_start.as<uint32_t>(),
+                       I.cand_qid.as<uint32_t>(), (unsigned long long)cap);
+    HIP_CHECK(hipGetLastError());
+  };
+  if (dev_off) {
+    const uint32_t nparts = (nq + kern::kOffsetBlock - 1) / kern::kOffsetBlock;
+    I.offset_parts.Reserve((size_t)nparts * 8 + 8);
+    hipLaunchKernelGGL(kern::k_count_sums, dim3(nparts), dim3(256), 0, S(stream_), I.counts.as<uint32_t>(), nq,
+                       I.offset_parts.as<unsigned long long>());
+    hipLaunchKernelGGL(kern::k_count_scan, dim3(1), dim3(1024), 0, S(stream_),
+                       I.offset_parts.as<unsigned long long>(), nparts, (unsigned long long *)nullptr);
+    hipLaunchKernelGGL(kern::k_count_offsets, dim3(nparts), dim3(256), 0, S(stream_), I.counts.as<uint32_t>(), nq,
+                       I.offset_parts.as<unsigned long long>(), I.offsets.as<unsigned long long>());
+    HIP_CHECK(hipGetLastError());
+    if (cand_cap) launch_compact(cand_cap);
+  }
   TraceMark("k1b_enq");
-  HIP_CHECK(hipStreamSynchronize(S(stream_)));
+  HIP_CHECK(hipEventSynchronize(I.ev_nb));
   TraceMark("k1b_done");
   // counts into the host vector, offsets into it and into page-locked staging
   // (uploaded by DMA), in parts on the worker threads: the GPU waits for this
@@ -934,15 +972,17 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
       if (c == 3) wide_goff.push_back(goff[(size_t)(std::lower_bound(cls[3].begin(), cls[3].end(), qi) - cls[3].begin())]);
     }
   I.ncand = total;
+  // the device copy stands when its offsets were the final ones (no overflow)
+  // and it had room for every candidate
+  const bool redo_copy = !dev_off || overflow || total + 1 > cand_cap;
   I.cand_start.Reserve(total * 4 + 4);
   I.cand_qid.Reserve(total * 4 + 4);
-  HIP_CHECK(hipMemcpyAsync(I.offsets.p, h_off, (size_t)nq * 8, hipMemcpyHostToDevice, S(stream_)));
-  // slot -> compact
-  hipLaunchKernelGGL(kern::k_compact, dim3((nq + 3) / 4), dim3(256), 0, S(stream_),
-                     I.slots.as<uint32_t>(), slot_cap, I.counts.as<uint32_t>(), (const uint8_t *)nullptr,
-                     I.offsets.as<unsigned long long>(), nq, I.cand_start.as<uint32_t>(),
-                     I.cand_qid.as<uint32_t>());
-  HIP_CHECK(hipGetLastError());
+  if (redo_copy) {
+    if (!dev_off || overflow)
+      HIP_CHECK(hipMemcpyAsync(I.offsets.p, h_off, (size_t)nq * 8, hipMemcpyHostToDevice, S(stream_)));
+    launch_compact(total + 1);  // slot -> compact
+  }
+  times_.seed_compact_redo += dev_off && redo_copy ? 1 : 0;
   // pass 2: queries with more candidates than a slot, written straight into place
   size_t nwide = 0;
   for (auto &v : wide) nwide += v.size();
@@ -1224,19 +1264,34 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
   // the next segment's tasks, built on the host while K2 runs and uploaded on
   // the copy stream into the other buffer (its last reader, the previous K2,
   // has finished: ScoreFinish waited for it)
+  // (the pipelined caller defers it, ScoreDeferNext, and builds it with
+  // ScorePrepareNext after it has enqueued this segment's K4/K3, so the build
+  // overlaps them too)
+  I.deferred = Impl::DeferredNext{};
   if (next && next->n) {
-    const int nb = I.task_turn;
-    PinnedBuf &hs = I.h_tasks[nb];
-    int nkind = kScoreRows;
-    hs.Reserve(task_bytes(next->n, next->q_first, next->q_end));
-    const size_t nt = BuildTasks(swar, next->cand_begin, next->n, next->q_first, next->q_end, counts, offsets,
-                                 per_block, hs.as<kern::ScoreTask>(), &nkind, guard == 0);
-    const size_t nbytes = nt * (nkind == kScorePairs ? 4 : sizeof(kern::ScoreTask));
-    I.task_buf[nb].Reserve(nbytes);
-    HIP_CHECK(hipMemcpyAsync(I.task_buf[nb].p, hs.p, nbytes, hipMemcpyHostToDevice, S(copy_stream_)));
-    HIP_CHECK(hipEventRecord(I.ev_tasks, S(copy_stream_)));
-    I.prepared = Impl::Prepared{true, next->cand_begin, next->n, (uint32_t)nt, per_block, swar, nkind, nb};
+    I.deferred = Impl::DeferredNext{true, *next, swar, guard == 0, per_block,
+                                    task_bytes(next->n, next->q_first, next->q_end)};
+    if (!defer_next_) ScorePrepareNext(counts, offsets);
   }
+}
+
+void DeviceModule::ScorePrepareNext(const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets) {
+  Impl &I = *impl_;
+  if (!I.deferred.valid) return;
+  const Impl::DeferredNext dn = I.deferred;
+  I.deferred.valid = false;
+  const ScoreSegment *next = &dn.seg;
+  const int nb = I.task_turn;
+  PinnedBuf &hs = I.h_tasks[nb];
+  int nkind = kScoreRows;
+  hs.Reserve(dn.bytes);
+  const size_t nt = BuildTasks(dn.swar, next->cand_begin, next->n, next->q_first, next->q_end, counts, offsets,
+                               dn.per_block, hs.as<kern::ScoreTask>(), &nkind, dn.pairs_ok);
+  const size_t nbytes = nt * (nkind == kScorePairs ? 4 : sizeof(kern::ScoreTask));
+  I.task_buf[nb].Reserve(nbytes);
+  HIP_CHECK(hipMemcpyAsync(I.task_buf[nb].p, hs.p, nbytes, hipMemcpyHostToDevice, S(copy_stream_)));
+  HIP_CHECK(hipEventRecord(I.ev_tasks, S(copy_stream_)));
+  I.prepared = Impl::Prepared{true, next->cand_begin, next->n, (uint32_t)nt, dn.per_block, dn.swar, nkind, nb};
 }
 
 bool DeviceModule::ScoreGuarded() const { return impl_ && impl_->score_state.active && impl_->score_state.guarded; }

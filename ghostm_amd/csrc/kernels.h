@@ -1089,16 +1089,103 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   RankEmitted<BLOCK>(a, q, s_emit, total);
 }
 
-// Slot -> compact copy for queries whose candidates fit their slot.
+// Device offsets of K1's per-query counts (exclusive prefix, 64-bit), so the
+// compaction runs without waiting for the host: k_count_sums adds each block's
+// kOffsetBlock counts, k_count_scan turns the block sums into block prefixes (one
+// workgroup), k_count_offsets writes each query's offset. A kOverflow count (a
+// query the host redoes) counts 0 here; the host then recomputes the offsets.
+constexpr uint32_t kOffsetBlock = 1024;  // counts per block: 256 threads x 4
+__device__ inline uint32_t CountOf(const uint32_t *counts, uint32_t i, uint32_t nq) {
+  const uint32_t c = i < nq ? counts[i] : 0u;
+  return c == kOverflow ? 0u : c;
+}
+__device__ inline unsigned long long WaveInclusiveScan64(unsigned long long x) {
+  const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned long long y = __shfl_up(x, d);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  return x;
+}
+__global__ __launch_bounds__(256) void k_count_sums(const uint32_t *counts, uint32_t nq, unsigned long long *part) {
+  GHOSTM_POISON_LDS();
+  __shared__ unsigned long long s_w[4];
+  const uint32_t i0 = blockIdx.x * kOffsetBlock + threadIdx.x * 4;
+  unsigned long long v = 0;
+  for (uint32_t k = 0; k < 4; ++k) v += CountOf(counts, i0 + k, nq);
+  for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+__global__ __launch_bounds__(1024) void k_count_scan(unsigned long long *part, uint32_t nparts,
+                                                     unsigned long long *total) {
+  GHOSTM_POISON_LDS();
+  __shared__ unsigned long long s_w[16];
+  __shared__ unsigned long long s_carry;
+  if (threadIdx.x == 0) s_carry = 0;
+  __syncthreads();
+  for (uint32_t base = 0; base < nparts; base += 1024) {
+    const uint32_t i = base + threadIdx.x;
+    const unsigned long long v = i < nparts ? part[i] : 0ull;
+    const unsigned long long x = WaveInclusiveScan64(v);
+    if ((threadIdx.x & 63) == 63) s_w[threadIdx.x >> 6] = x;
+    __syncthreads();
+    unsigned long long before = s_carry;
+    for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) before += s_w[w];
+    if (i < nparts) part[i] = before + x - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) s_carry = before + x;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && total) *total = s_carry;
+}
+__global__ __launch_bounds__(256) void k_count_offsets(const uint32_t *counts, uint32_t nq,
+                                                       const unsigned long long *part, unsigned long long *offsets) {
+  GHOSTM_POISON_LDS();
+  __shared__ unsigned long long s_w[4];
+  const uint32_t i0 = blockIdx.x * kOffsetBlock + threadIdx.x * 4;
+  uint32_t c[4];
+  unsigned long long v = 0;
+  for (uint32_t k = 0; k < 4; ++k) {
+    c[k] = CountOf(counts, i0 + k, nq);
+    v += c[k];
+  }
+  const unsigned long long x = WaveInclusiveScan64(v);
+  if ((threadIdx.x & 63) == 63) s_w[threadIdx.x >> 6] = x;
+  __syncthreads();
+  unsigned long long o = part[blockIdx.x] + x - v;
+  for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) o += s_w[w];
+  for (uint32_t k = 0; k < 4; ++k) {
+    if (i0 + k < nq) offsets[i0 + k] = o;
+    o += c[k];
+  }
+}
+
+// Test knob (GHOSTM_K1_FORCE_OVERFLOW=k): every k-th query of the LDS classes
+// (0 < bins <= lds_cap) reports a filter-queue overflow, so the host's redo path
+// (unfiltered table, host offsets, a second compaction) runs on small datasets.
+__global__ void k_force_overflow(uint32_t *counts, const uint32_t *nbins, uint32_t nq, uint32_t every,
+                                 uint32_t lds_cap) {
+  GHOSTM_POISON_LDS();
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < nq && q % every == 0 && nbins[q] > 0 && nbins[q] <= lds_cap) counts[q] = kOverflow;
+}
+
+// Slot -> compact copy for queries whose candidates fit their slot. Nothing is
+// written past `cap` candidates (the device offsets are computed before the host
+// has seen the total; it re-runs the copy when the buffers had to grow).
 __global__ void k_compact(const uint32_t *slots, uint32_t slot_cap, const uint32_t *counts,
                           const uint8_t *in_slot, const unsigned long long *offsets,
-                          uint32_t nq, uint32_t *out_start, uint32_t *out_qid) {
+                          uint32_t nq, uint32_t *out_start, uint32_t *out_qid, unsigned long long cap) {
   GHOSTM_POISON_LDS();
   const uint32_t q = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   if (q >= nq) return;
   const uint32_t c = counts[q];
   if ((in_slot && !in_slot[q]) || c > slot_cap) return;
   const unsigned long long o = offsets[q];
+  if (o + c > cap) return;
   for (uint32_t i = threadIdx.x & 63; i < c; i += 64) {
     out_start[o + i] = slots[(size_t)q * slot_cap + i];
     out_qid[o + i] = q;

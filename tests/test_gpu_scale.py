@@ -79,6 +79,22 @@ def test_every_k1_class_and_the_offset_pass(k1, ds, var, opts, dataset, golden):
     assert dev.tobytes() == hits.tobytes()
 
 
+@pytest.mark.parametrize("devoff", ["1", "0"])
+@pytest.mark.parametrize("ds,var,opts", [("syn_small", "default", []), ("syn_dna", "default", []),
+                                         ("syn_scale", "default", []), ("syn_chunks", "default", [])])
+def test_k1_overflow_redo_and_device_offsets(devoff, ds, var, opts, dataset, golden):
+    """K1's filter-queue overflow path, forced on every third query of the LDS
+    classes (GHOSTM_K1_FORCE_OVERFLOW): the unfiltered table redoes them, the host
+    offsets replace the device ones and the compaction runs again; with the
+    device offsets on (default) and off (GHOSTM_K1_DEVOFF=0). Same bytes as the
+    reference."""
+    d = dataset(ds)
+    text, st, hits, dev = _run(d, opts, {"GHOSTM_K1_FORCE_OVERFLOW": "3", "GHOSTM_K1_DEVOFF": devoff})
+    assert _sha(text) == golden["aln"][f"{ds}/{var}"]["sha256"]
+    assert st["seed_filter_overflows"] > 0, st
+    assert dev.tobytes() == hits.tobytes()
+
+
 def test_syn_scale_runs_the_cfg4_classes(dataset, golden):
     """The cfg4 generator's DB with its first 5000 queries, default options: K1
     classes 1 and 2 (k_seed_hash<512,12288>, <1024,24576>) and the offset pass
