@@ -509,7 +509,8 @@ def main() -> None:
                            "back first; H2D; N > 1: rank-local reads and the "
                            "batch-plan all-gather), the search, text formatting and the output file write "
                            "(N = 1: written while the search runs; N > 1: every rank writes its slice of the "
-                           "one file)"}
+                           "one file); sessions run one after another in this process, which keeps device "
+                           "blocks from the previous session (DevPool)"}
         if rank == 0:
             e2e["output_files_match_reference" if pin else "output_files_match_timed_run"] = all(files_ok)
             if not all(files_ok):

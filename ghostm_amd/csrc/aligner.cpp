@@ -507,8 +507,14 @@ void Session::PlanExchange(uint32_t rank, uint32_t world, const ShardExchange &e
   }
 }
 
-std::vector<Batch> Session::Passes(QueryData &q, size_t di, const std::vector<uint32_t> &counts) const {
-  if (!q.planned) return CpuBatches(counts, opt_.max_list_length);
+std::vector<Batch> Session::Passes(QueryData &q, size_t di, const std::vector<uint32_t> &counts,
+                                   uint64_t total) const {
+  if (!q.planned) {
+    // within -l the rule makes one batch (none without candidates): no scan
+    if (total <= opt_.max_list_length)
+      return total ? std::vector<Batch>{Batch{0, (uint32_t)counts.size()}} : std::vector<Batch>{};
+    return CpuBatches(counts, opt_.max_list_length);
+  }
   uint64_t sum = 0;
   for (uint32_t c : counts) sum += c;
   if (di >= q.plan.size() || sum != q.plan_sum[di] || CountsHash(counts.data(), counts.size()) != q.plan_hash[di])
@@ -921,8 +927,16 @@ void Session::DevicePass(QueryData &q, DbData &d, const std::vector<uint32_t> &c
     uint64_t target = rem > 2 * kSegmentCands || !final_pass ? kSegmentCands
                                                               : std::max<uint64_t>(kTailCands, rem * 3 / 5);
     if (g0 == gb0 && kHeadCands && rem > 2 * kHeadCands) target = std::min(target, kHeadCands);
-    uint32_t g1 = g0 + 1;
-    while (g1 < gb1 && group_begin(g1) - group_begin(g0) < target) ++g1;
+    // the first group g1 > g0 at least `target` candidates on (group_begin
+    // does not decrease with g: a binary search, not a walk over the groups)
+    const uint64_t from = group_begin(g0);
+    uint32_t lo = g0 + 1, hi = gb1;
+    while (lo < hi) {
+      const uint32_t mid = lo + (hi - lo) / 2;
+      if (group_begin(mid) - from < target) lo = mid + 1;
+      else hi = mid;
+    }
+    const uint32_t g1 = lo;
     cuts.emplace_back(g0, g1);
     g0 = g1;
   }
@@ -973,6 +987,11 @@ void Session::DevicePass(QueryData &q, DbData &d, const std::vector<uint32_t> &c
       PartDone(part);
     });
   };
+  struct DeferNext {  // ScorePrepareNext below builds each next segment's tasks
+    DeviceModule &dev;
+    explicit DeferNext(DeviceModule &d) : dev(d) { dev.ScoreDeferNext(true); }
+    ~DeferNext() { dev.ScoreDeferNext(false); }
+  } defer_next{dev};
   for (size_t k = 0; k < cuts.size(); ++k) {
     const uint32_t g0 = cuts[k].first, g1 = cuts[k].second;
     const uint64_t c0 = segs[k].cand_begin, c1 = c0 + segs[k].n;
@@ -994,6 +1013,8 @@ void Session::DevicePass(QueryData &q, DbData &d, const std::vector<uint32_t> &c
       dev.MergeLaunch(q.dev, d.dev, g0, g1, c0, c1 - c0, opt_.best, tb_base, opt_.open_gap, opt_.extend_gap, pass);
       pending = Pending{g0, g1, true, false};
     }
+    // segment k + 1's K2 tasks, while K2(k) and K4/K3(k) run
+    dev.ScorePrepareNext(counts, offsets);
     dev.ScoreFinish();
     TraceMark("score_done", c1 - c0);
     if (work && guarded) {
@@ -1059,7 +1080,7 @@ void Session::RunQueryChunk(QueryData &q) {
     TraceMark("seed_done", total);
     // (a shard replays the unsharded run's batches; those that miss its
     // queries are passes without candidates over its carried lists)
-    const std::vector<Batch> batches = Passes(q, di, counts);
+    const std::vector<Batch> batches = Passes(q, di, counts, total);
     TraceMark("batches", batches.size());
     for (size_t bi = 0; bi < batches.size(); ++bi) {
       const Batch &b = batches[bi];

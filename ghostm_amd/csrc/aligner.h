@@ -189,7 +189,9 @@ class Session {
                     const std::vector<uint32_t> &chunk_nseq, const std::vector<std::vector<uint64_t>> &rank_lo);
   // the passes of one Seed() result: the plan's batches restricted to the
   // slice (local indices, possibly empty), or the slice's own cuts unsharded
-  std::vector<Batch> Passes(QueryData &q, size_t di, const std::vector<uint32_t> &counts) const;
+  // (total: the counts' sum when known, else UINT64_MAX)
+  std::vector<Batch> Passes(QueryData &q, size_t di, const std::vector<uint32_t> &counts,
+                            uint64_t total = UINT64_MAX) const;
   void RunQueryChunk(QueryData &q);
   void RunQueryChunkHostMerge(QueryData &q);
   void DevicePass(QueryData &q, DbData &d, const std::vector<uint32_t> &counts,
