@@ -897,8 +897,13 @@ void Session::DevicePass(QueryData &q, DbData &d, const std::vector<uint32_t> &c
   if (const char *e = getenv("GHOSTM_TAIL_CANDS")) kTailCands = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
   // the first segment's K2 tasks are built while the GPU waits (the later
   // ones during the previous K2): a head of at most kHeadCands shortens that
-  // wait (GHOSTM_HEAD_CANDS; 0 = no head cap)
-  uint64_t kHeadCands = kTailCands;
+  // wait (GHOSTM_HEAD_CANDS; 0 = no head cap). At >= 96 candidates per query the
+  // unit kernel's consecutive tasks need no count pass (score_tasks.h) and the
+  // build is short (0.04 ms for the 125 K-query shard's first 1 M): no head
+  // there, one segment fewer (shard 46.5-46.8 against 46.7-47.5 ms with it,
+  // profiles/r5t/)
+  const uint64_t batch_queries = bq1 > bq0 ? bq1 - bq0 : 1;
+  uint64_t kHeadCands = (c_hi - c_lo) / batch_queries >= 96 ? 0 : kTailCands;
   if (const char *e = getenv("GHOSTM_HEAD_CANDS")) kHeadCands = strtoull(e, nullptr, 10);
   const uint32_t ng = (uint32_t)q.group_first.size();
   // a group's first candidate of this batch (groups outside it have none)
