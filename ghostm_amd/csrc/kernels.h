@@ -2446,6 +2446,15 @@ struct TbArgs {
 };
 constexpr uint32_t kTbStripClasses = 4;
 
+// K3 work in longest-first order (GHOSTM_K3_LPT=1: the scan's persistent loop
+// from the widest pairs down, the key DP's waves from the last class and the
+// most columns down). Measured (profiles/r5ab/): the scan unchanged, the key DP
+// 6.60 -> 6.43 ms per cfg5 step but 18.55 -> 19.15 at cfg4 and 2.28 -> 2.52 at
+// cfg3, so ascending order stays the default.
+#ifndef GHOSTM_K3_LPT
+#define GHOSTM_K3_LPT 0
+#endif
+
 // the wave's largest value (loop bound of a lane-group loop)
 __device__ inline uint32_t WaveMax(uint32_t v) {
   for (int d = 32; d > 0; d >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, d));
@@ -2604,8 +2613,23 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
 
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // strip classes (FINAL, class_off): the waves of class c come after those of
-  // classes < c, each running 64 / (c + 1) hits in groups of c + 1 lanes
+  // classes < c, each running 64 / (c + 1) hits in groups of c + 1 lanes.
+  // Waves are taken from the end (KEY_LPT): the longest hits (the last class,
+  // the most columns) are dispatched first, the short ones fill the tail
   uint32_t G = a.G, gpw = a.gpw, wv = blockIdx.x * (kTbBlock / 64) + wave, lo = 0, hi = a.n;
+  if constexpr (GHOSTM_K3_LPT) {
+    uint32_t total = 0;
+    if (FINAL && a.class_off) {
+      for (uint32_t c = 0; c < kTbStripClasses; ++c) {
+        const uint32_t gp = 64 / (c + 1);
+        total += (a.class_off[c + 1] - a.class_off[c] + gp - 1) / gp;
+      }
+    } else {
+      total = (a.n + a.gpw - 1) / a.gpw;
+    }
+    if (wv >= total) return;  // past the last wave (no barrier below)
+    wv = total - 1 - wv;
+  }
   if (FINAL && a.class_off) {
     uint32_t c = 0;
     for (; c < kTbStripClasses; ++c) {
@@ -3532,9 +3556,13 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
   const uint32_t stride = gridDim.x * (kScanBlock / 64) * a.gpw;
   const C cell(a.open, a.ext);
   for (uint32_t first = (blockIdx.x * (kScanBlock / 64) + wave) * a.gpw; first < nitems; first += stride) {
-    const uint32_t it = first + g;
+    // this wave's items [lo, hi): counted from the end (GHOSTM_K3_LPT, the
+    // widest first) or from the start
+    const uint32_t lo = GHOSTM_K3_LPT ? (first + a.gpw > nitems ? 0u : nitems - first - a.gpw) : first;
+    const uint32_t hi = GHOSTM_K3_LPT ? nitems - first : min(first + a.gpw, nitems);
+    const uint32_t it = lo + g;
     uint32_t sA = 0xFFFFFFFFu, sB = 0xFFFFFFFFu, wA = 0, wB = 0, p0A = 0, p0B = 0, q = 0;
-    if (g < a.gpw && it < nitems) {
+    if (g < a.gpw && it < hi) {
       const uint32_t item = a.items[it];
       sA = a.pair_a[item];
       sB = a.pair_b[item];
@@ -3606,7 +3634,7 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
     const uint32_t clA = (wA ? wA : 1u) - 1, clB = (wB ? wB : 1u) - 1;
     // items ascend by key = max(wA, wB): the batch's last item has the longest
     // window (a clamped key stands for the whole window)
-    const uint32_t last = a.items[min(first + a.gpw, nitems) - 1];
+    const uint32_t last = a.items[hi - 1];
     uint32_t wmax = __builtin_amdgcn_readfirstlane(a.key[last]);  // key of an item index
     if (wmax >= kSortBins - 1) wmax = a.base;
     const uint32_t steps = wmax + a.G - 1;
