@@ -306,7 +306,7 @@ void Session::PrepareQueryChunk(QueryData *qd, bool qlen) {
 // blocks of rows (a row's last byte per 127: ~9 ms per 500 K-query chunk on one
 // thread, the largest part of reading a chunk once its names are a NameTable).
 void Session::QueryLengths(std::vector<QueryData *> chunks) {
-  constexpr uint32_t kRows = 1u << 15;
+  constexpr uint32_t kRows = 1u << 12;
   std::vector<std::pair<QueryData *, uint32_t>> blocks;
   for (QueryData *q : chunks) {
     q->qlen.assign(q->chunk.nseq, 1);
@@ -646,17 +646,50 @@ void Session::Load(uint32_t shard_rank, uint32_t shard_world, bool local, std::v
   std::vector<DbData> dread(nd_chunks);
   std::vector<char> qok(nq_chunks, 0), dok(nd_chunks, 0);
   // (each query chunk's name groups and WriteOutput lengths are derived on its
-  // reading thread too; a rank-local shard only indexes the query chunks here)
+  // reading thread too; a rank-local shard only indexes the query chunks here).
+  // A DB chunk is uploaded by its reading thread as soon as it is read, one
+  // upload at a time (the staging buffers are shared), while the query chunks
+  // are still being read (cfg3: the 34 MB DB and index upload took 1.5 ms of a
+  // 4.1 ms session create after every read, profiles/r5ad/)
+  std::mutex upload_mu;
+  auto upload_db = [&](DbData &d) {
+    std::lock_guard<std::mutex> lock(upload_mu);
+    const DbChunk &c = d.chunk;
+    d.dev = dev.UploadDb(c.seq.data(), c.len, c.keys_count.data(), c.kcl, c.positions.data(), c.npos);
+    if (c.nseq) dev.SetDbSubjects(d.dev, c.starts.data(), c.nseq);
+    // resident on the device from here; the host keeps names and starts
+    d.chunk.seq.Release();
+    d.chunk.keys_count.Release();
+    d.chunk.positions.Release();
+  };
+  auto upload_query = [&](QueryData &q) {
+    std::lock_guard<std::mutex> lock(upload_mu);
+    q.dev = dev.UploadQuery(q.chunk.seq.data(), q.chunk.nseq, q.chunk.L);
+    dev.SetQueryGroups(q.dev, q.group_first.data(), q.group_last.data(), (uint32_t)q.group_first.size());
+  };
   ParallelFor(nq_chunks + nd_chunks, std::max<unsigned>(1u, std::min(threads_, 8u)),
-              [&](size_t b, size_t e, unsigned) {
-                for (size_t k = b; k < e; ++k) {
+              [&](size_t b0, size_t e0, unsigned) {
+                // DB chunks first (they are listed after the query chunks)
+                for (size_t j = b0; j < e0; ++j) {
+                  const size_t k = nq_chunks + nd_chunks - 1 - j;
                   if (k < nq_chunks && local) {
                     qok[k] = qf.IndexChunk(id + (uint32_t)k, &qidx[k]);
                   } else if (k < nq_chunks) {
                     qok[k] = qf.ReadChunk(id + (uint32_t)k, &qread[k].chunk);
                     if (qok[k]) PrepareQueryChunk(&qread[k], false);
+                    TraceMark("q_chunk_read", k);
+                    // an unsharded session uploads the chunk here too (a sharded
+                    // one keeps only its slice, below)
+                    if (qok[k] && shard_world == 1) {
+                      upload_query(qread[k]);
+                      TraceMark("q_chunk_up", k);
+                    }
                   } else {
-                    dok[k - nq_chunks] = df.ReadChunk((uint32_t)(k - nq_chunks), &dread[k - nq_chunks].chunk);
+                    DbData &d = dread[k - nq_chunks];
+                    dok[k - nq_chunks] = df.ReadChunk((uint32_t)(k - nq_chunks), &d.chunk);
+                    TraceMark("db_chunk_read", k - nq_chunks);
+                    if (dok[k - nq_chunks]) upload_db(d);
+                    TraceMark("db_chunk_up", k - nq_chunks);
                   }
                 }
               });
@@ -672,22 +705,16 @@ void Session::Load(uint32_t shard_rank, uint32_t shard_world, bool local, std::v
 
   db_sum_u32_ = (uint32_t)df.sum_length;
   uint32_t dbase = 0;
-  for (uint32_t k = 0; k < nd_chunks && dok[k]; ++k) {
-    dread[k].global_base = dbase;
-    dbase += dread[k].chunk.nseq;
-    dbs_.push_back(std::move(dread[k]));
+  uint32_t nd_kept = 0;
+  for (; nd_kept < nd_chunks && dok[nd_kept]; ++nd_kept) {
+    dread[nd_kept].global_base = dbase;
+    dbase += dread[nd_kept].chunk.nseq;
+    dbs_.push_back(std::move(dread[nd_kept]));
   }
+  for (uint32_t k = nd_kept; k < nd_chunks; ++k)  // read past a missing chunk: not used
+    if (dread[k].dev) dev.Free(dread[k].dev);
   if (dbs_.empty()) throw std::runtime_error("[Aligner] error: don't find db file.");
   TraceMark("db_read", dbs_.size());
-  for (DbData &d : dbs_) {
-    const DbChunk &c = d.chunk;
-    d.dev = dev.UploadDb(c.seq.data(), c.len, c.keys_count.data(), c.kcl, c.positions.data(), c.npos);
-    if (c.nseq) dev.SetDbSubjects(d.dev, c.starts.data(), c.nseq);
-    // resident on the device from here; the host keeps names and starts
-    d.chunk.seq.Release();
-    d.chunk.keys_count.Release();
-    d.chunk.positions.Release();
-  }
   {
     std::vector<uint32_t> bases;
     for (const DbData &d : dbs_) bases.push_back(d.global_base);
@@ -754,11 +781,11 @@ void Session::Load(uint32_t shard_rank, uint32_t shard_world, bool local, std::v
   }
 
   for (QueryData &q : queries_) {
-    const uint32_t n = q.chunk.nseq, L = q.chunk.L;
-    q.dev = dev.UploadQuery(q.chunk.seq.data(), n, L);
-    dev.SetQueryGroups(q.dev, q.group_first.data(), q.group_last.data(), (uint32_t)q.group_first.size());
+    if (!q.dev) upload_query(q);  // (uploaded while reading when unsharded)
     q.chunk.seq.Release();  // resident on the device (qlen and names stay on the host)
   }
+  for (uint32_t k = nchunks; k < nq_chunks; ++k)  // read past a missing chunk: not used
+    if (qread[k].dev) dev.Free(qread[k].dev);
 }
 
 namespace {

@@ -30,8 +30,16 @@ bool FileArray<T>::Map(const std::string &path, uint64_t off, size_t n) {
     const uint64_t page = (uint64_t)sysconf(_SC_PAGESIZE);
     const uint64_t first = off / page * page;
     const size_t len = (size_t)(off + bytes - first);
-    void *m = mmap(nullptr, len, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, (off_t)first);
+    // the page tables filled by the threads that read the mapping (the staged
+    // upload's copies and the query-length pass run on the worker pool), not
+    // up front by this one (MAP_POPULATE); GHOSTM_MAP_POPULATE=1 restores it (A/B)
+    static const bool populate = [] {
+      const char *e = getenv("GHOSTM_MAP_POPULATE");
+      return e && strcmp(e, "1") == 0;
+    }();
+    void *m = mmap(nullptr, len, PROT_READ, MAP_PRIVATE | (populate ? MAP_POPULATE : 0), fd, (off_t)first);
     if (m != MAP_FAILED) {
+      if (!populate) madvise(m, len, MADV_WILLNEED);
       hold_ = std::shared_ptr<const void>(m, [len](const void *q) { munmap(const_cast<void *>(q), len); });
       p_ = reinterpret_cast<const T *>(static_cast<const char *>(m) + (off - first));
       n_ = n;
@@ -228,9 +236,19 @@ bool QueryFile::ReadChunk(uint32_t id, QueryChunk *q) const {
 }
 
 uint32_t QueryResidues(const uint8_t *s, uint32_t L) {
-  uint32_t e = L - 1;
-  while (e > 0 && s[e] == kBaseX) --e;
-  return e + 1;
+  // the last byte that is not padding, eight bytes at a time from the end
+  constexpr uint64_t kPad8 = 0x0101010101010101ull * kBaseX;
+  uint32_t e = L;
+  while (e >= 9) {
+    uint64_t w;
+    std::memcpy(&w, s + e - 8, 8);
+    const uint64_t x = w ^ kPad8;
+    if (x) return e - 8 + (uint32_t)(63 - __builtin_clzll(x)) / 8 + 1;
+    e -= 8;
+  }
+  uint32_t k = e - 1;
+  while (k > 0 && s[k] == kBaseX) --k;
+  return k + 1;
 }
 
 bool QueryFile::IndexChunk(uint32_t id, QueryChunkIndex *q) const {
