@@ -229,7 +229,7 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=None,
                     help="ranks (one process per GPU); without WORLD_SIZE, N > 1 starts them itself")
     ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--preset", choices=sorted(workloads.WORKLOADS), default="cfg4",
                     help="BASELINE.json config (cfg4 = the headline workload)")
     ap.add_argument("--queries", type=int, default=None, help="queries of the whole job (default: preset)")

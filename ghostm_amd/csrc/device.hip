@@ -259,7 +259,7 @@ struct DeviceModule::Impl {
   bool matrix_set = false;
 };
 
-static constexpr uint32_t kSlotCap = 256;
+static constexpr uint32_t kSlotCap = kern::kMaxSlotCap;
 // Filtered slot pass (k_seed_filter) of classes 0, 1 and 2, thresholds >= 2:
 // <BLOCK, filter cells, table slots, queue, alias> and its dynamic LDS bytes.
 // The bitmap shares its LDS with the exact table (alias), which doubled the

@@ -76,7 +76,12 @@ __device__ inline uint32_t ShiftUp(uint32_t v) {
 
 constexpr uint32_t kMaxLists = 128;
 constexpr uint32_t kOverflow = 0xFFFFFFFFu;
-constexpr uint32_t kMaxSlotCap = 256;  // slot pass: candidates per query slot
+// slot pass: candidates per query slot; a query with more is redone by the
+// merge kernel in offset mode (GHOSTM_K1_SLOT=256 builds the earlier size, A/B)
+#ifndef GHOSTM_K1_SLOT
+#define GHOSTM_K1_SLOT 512
+#endif
+constexpr uint32_t kMaxSlotCap = GHOSTM_K1_SLOT;
 
 struct SeedListArgs {
   const uint8_t *qseq;
