@@ -918,8 +918,15 @@ void Session::DevicePass(QueryData &q, DbData &d, const std::vector<uint32_t> &c
   // formatting overlaps the next one's K2 (cfg2's 0.9 M: 10.2 -> 8.7 ms per
   // step; at cfg3 and the 125 K shard a smaller floor only adds launches,
   // profiles/r4_tail_sweep.txt)
+  // The floor's cap counts the last segment's formatting, which grows with its
+  // queries, not its candidates: 1 M candidates or 16 K queries' worth,
+  // whichever is more (dense batches, 127 per query: ~2 M; cfg4 351.1 -> 350.5
+  // ms, the 125 K shard 46.7 -> 46.4 ms; cfg3's 63 per query keeps ~1 M: 2 M
+  // lost 0.5 ms there, profiles/r5aj/, profiles/r5ai/)
+  const uint64_t batch_q = bq1 > bq0 ? bq1 - bq0 : 1;
+  const uint64_t tail_cap = std::max<uint64_t>(1ull << 20, (c_hi - c_lo) / batch_q * 16384);
   uint64_t kSegmentCands = 16ull << 20;
-  uint64_t kTailCands = std::min<uint64_t>(1ull << 20, std::max<uint64_t>(1ull << 17, (c_hi - c_lo) / 4));
+  uint64_t kTailCands = std::min<uint64_t>(tail_cap, std::max<uint64_t>(1ull << 17, (c_hi - c_lo) / 4));
   if (const char *e = getenv("GHOSTM_SEGMENT_CANDS")) kSegmentCands = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
   if (const char *e = getenv("GHOSTM_TAIL_CANDS")) kTailCands = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
   // the first segment's K2 tasks are built while the GPU waits (the later
@@ -929,8 +936,7 @@ void Session::DevicePass(QueryData &q, DbData &d, const std::vector<uint32_t> &c
   // build is short (0.04 ms for the 125 K-query shard's first 1 M): no head
   // there, one segment fewer (shard 46.5-46.8 against 46.7-47.5 ms with it,
   // profiles/r5t/)
-  const uint64_t batch_queries = bq1 > bq0 ? bq1 - bq0 : 1;
-  uint64_t kHeadCands = (c_hi - c_lo) / batch_queries >= 96 ? 0 : kTailCands;
+  uint64_t kHeadCands = (c_hi - c_lo) / batch_q >= 96 ? 0 : kTailCands;
   if (const char *e = getenv("GHOSTM_HEAD_CANDS")) kHeadCands = strtoull(e, nullptr, 10);
   const uint32_t ng = (uint32_t)q.group_first.size();
   // a group's first candidate of this batch (groups outside it have none)
