@@ -173,6 +173,7 @@ constexpr uint32_t kDbFront = kern::kDbFrontPad, kDbBack = 65536;
 
 struct DevDb {
   DevBuf seq, kc, pos;
+  DevBuf low;                      // kern::k_low_keys' bitmap
   uint32_t len = 0, kcl = 0, npos = 0;
   const uint8_t *Residues() const { return seq.as<uint8_t>() + kDbFront; }
   DevBuf subj;                     // subject starts (device merge)
@@ -528,6 +529,13 @@ DevDb *DeviceModule::UploadDb(const uint8_t *seq, uint32_t len, const uint32_t *
   StagedUpload(static_cast<uint8_t *>(d->seq.p) + kDbFront, seq, len);
   StagedUpload(d->kc.p, kc, (size_t)kcl * 4);
   StagedUpload(d->pos.p, pos, (size_t)npos * 4);
+  const uint32_t nkeys = kcl ? kcl - 1 : 0;
+  d->low.Reserve(((size_t)nkeys + 63) / 64 * 8 + 8);
+  if (nkeys) {
+    hipLaunchKernelGGL(kern::k_low_keys, dim3((nkeys + 255) / 256), dim3(256), 0, S(stream_), d->kc.as<uint32_t>(),
+                       d->pos.as<uint32_t>(), nkeys, d->low.as<unsigned long long>());
+    HIP_CHECK(hipGetLastError());
+  }
   return d;
 }
 
@@ -548,6 +556,7 @@ void DeviceModule::Free(DevDb *d) {
   d->seq.Release();
   d->kc.Release();
   d->pos.Release();
+  d->low.Release();
   d->subj.Release();
   d->subj_bucket.Release();
   delete d;
@@ -726,6 +735,7 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
   la.nq = nq;
   la.keys_count = d->kc.as<uint32_t>();
   la.positions = d->pos.as<uint32_t>();
+  la.low_keys = d->low.as<unsigned long long>();
   la.seed_mask = cfg.seed_mask;
   la.nlists = nlists;
   la.shift = cfg.shift;

@@ -88,11 +88,33 @@ struct SeedListArgs {
   uint32_t L, nq;
   const uint32_t *keys_count;
   const uint32_t *positions;
+  const unsigned long long *low_keys;  // k_low_keys' bitmap
   uint32_t seed_mask, nlists, shift;
   uint32_t *list_beg;             // [nq * nlists]
   uint32_t *list_len;             // [nq * nlists]
   uint32_t *nbins;                // [nq]
 };
+
+// Keys whose list starts below kLowLimit, one bit each (128 KB for 2^20 keys,
+// L2-resident): K1a reads a list's first position, a random line of the
+// positions array, only for these keys (the trim below is for lists with hits
+// in the first j*shift query residues, so a key with no such hit can skip it).
+// (GHOSTM_K1_LOWKEYS=0 builds the unfiltered read, A/B)
+#ifndef GHOSTM_K1_LOWKEYS
+#define GHOSTM_K1_LOWKEYS 1
+#endif
+constexpr uint32_t kLowLimit = GHOSTM_K1_LOWKEYS ? 1u << 12 : 0;
+__global__ __launch_bounds__(256) void k_low_keys(const uint32_t *keys_count, const uint32_t *positions,
+                                                  uint32_t nkeys, unsigned long long *low) {
+  const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+  bool bit = false;
+  if (k < nkeys) {
+    const uint32_t b = keys_count[k];
+    bit = b < keys_count[k + 1] && positions[b] < kLowLimit;
+  }
+  const unsigned long long m = __ballot(bit);
+  if ((threadIdx.x & 63) == 0 && k < nkeys) low[k >> 6] = m;
+}
 
 __global__ __launch_bounds__(256) void k_seed_lists(SeedListArgs a) {
   GHOSTM_POISON_LDS();
@@ -108,7 +130,8 @@ __global__ __launch_bounds__(256) void k_seed_lists(SeedListArgs a) {
       if (s & 1u) key = (key << 5) | qs[d0 + t];
     const uint32_t b = a.keys_count[key], e = a.keys_count[key + 1];
     uint32_t lo = b;
-    if (b < e && a.positions[b] < d0) {  // rare: hits in the first j*shift residues
+    const bool low = d0 > kLowLimit || ((a.low_keys[key >> 6] >> (key & 63)) & 1ull);
+    if (b < e && low && a.positions[b] < d0) {  // rare: hits in the first j*shift residues
       uint32_t hi = e;
       lo = b + 1;
       while (lo < hi) {
