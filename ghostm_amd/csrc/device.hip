@@ -524,11 +524,12 @@ DevDb *DeviceModule::UploadDb(const uint8_t *seq, uint32_t len, const uint32_t *
   d->npos = npos;
   d->seq.Reserve((size_t)kDbFront + len + kDbBack);
   d->kc.Reserve((size_t)kcl * 4);
-  d->pos.Reserve((size_t)npos * 4 + 4);
+  d->pos.Reserve(((size_t)npos + kern::kPosTailPad) * 4);
   HIP_CHECK(hipMemsetAsync(d->seq.p, (int)kern::kSeqEnd, (size_t)kDbFront + len + kDbBack, S(stream_)));
   StagedUpload(static_cast<uint8_t *>(d->seq.p) + kDbFront, seq, len);
   StagedUpload(d->kc.p, kc, (size_t)kcl * 4);
   StagedUpload(d->pos.p, pos, (size_t)npos * 4);
+  HIP_CHECK(hipMemsetAsync(static_cast<uint32_t *>(d->pos.p) + npos, 0, (size_t)kern::kPosTailPad * 4, S(stream_)));
   const uint32_t nkeys = kcl ? kcl - 1 : 0;
   d->low.Reserve(((size_t)nkeys + 63) / 64 * 8 + 8);
   if (nkeys) {

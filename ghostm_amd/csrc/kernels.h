@@ -82,6 +82,9 @@ constexpr uint32_t kOverflow = 0xFFFFFFFFu;
 #define GHOSTM_K1_SLOT 512
 #endif
 constexpr uint32_t kMaxSlotCap = GHOSTM_K1_SLOT;
+// Entries of zero past the DB's positions (DevDb::pos): k_seed_filter's entry
+// slots past a query's last entry read there (list 0's start + the slot index)
+constexpr uint32_t kPosTailPad = 16384;
 
 struct SeedListArgs {
   const uint8_t *qseq;
@@ -398,6 +401,20 @@ __global__ __launch_bounds__(BLOCK) void k_seed(SeedArgs a) {
 //     with more candidates only get their count here and are redone by k_seed in
 //     offset mode. Needs every bin + 2 < 2^21 (kHashBinLimit).
 __device__ inline uint32_t BinHash(uint32_t b) { return b * 2654435761u; }
+// HASH24: the bucket from full-rate 24-bit multiplies (v_mul_u32_u24) instead of
+// the quarter-rate v_mul_lo_u32 / v_mul_hi_u32 pair: h = b * C (low 32 bits),
+// bucket = ((h >> s) * buckets) >> (32 - s) with 2^s >= buckets, so the product
+// stays below 2^32. Bins are < 2^22 (kHashBinLimit + 1). Any hash gives the same
+// counts and output (the table only has to find its keys); GHOSTM_K1_HASH24=0
+// keeps the 32-bit multiplicative hash (A/B)
+#ifndef GHOSTM_K1_HASH24
+#define GHOSTM_K1_HASH24 0
+#endif
+__host__ __device__ constexpr uint32_t CeilLog2(uint32_t v) {
+  uint32_t l = 0;
+  while ((1u << l) < v) ++l;
+  return l;
+}
 constexpr uint32_t kHashBinLimit = 1u << 21;
 
 // Slot word: (bin + 1) << 11 | count << 3, low three bits zero; 0 = empty.
@@ -414,7 +431,16 @@ struct BinTable {
   static constexpr uint32_t kBuckets = TSLOTS / 4;
   uint32_t *tab;
   __device__ static uint32_t Key(uint32_t b) { return (b + 1) << 11; }
-  __device__ static uint32_t Bucket(uint32_t b) { return __umulhi(BinHash(b), kBuckets); }
+  __device__ static uint32_t Bucket(uint32_t b) {
+    if constexpr (GHOSTM_K1_HASH24) {
+      constexpr uint32_t kS = CeilLog2(kBuckets);
+      static_assert(kS >= 8 && kS < 24, "(h >> s) and the bucket count fit 24 bits");
+      const uint32_t h = __umul24(b, 0x9E3779u);
+      return __umul24(h >> kS, kBuckets) >> (32 - kS);
+    } else {
+      return __umulhi(BinHash(b), kBuckets);
+    }
+  }
   __device__ static uint32_t Next(uint32_t k) { return k + 1 == kBuckets ? 0u : k + 1; }
   __device__ static uint32_t Min8(const uint32_t v[8]) {
     return min(min(min(v[0], v[1]), v[2]), min(min(min(v[3], v[4]), v[5]), min(v[6], v[7])));
@@ -663,6 +689,23 @@ __host__ __device__ constexpr uint32_t FilterWords(uint32_t fslots) { return fsl
 #ifndef GHOSTM_K1_BATCH
 #define GHOSTM_K1_BATCH 1
 #endif
+// Pass 1: every lane loads its entry's list predecessor itself (the same lines
+// as the entries; no lane-0 branch, no DPP) and the seen-twice marks go without
+// a branch: 6 fewer VALU instructions per entry slot, the class-1 launch 10.83
+// -> 10.22 ms, K1 25.7-25.9 -> 24.3-24.8 ms per cfg4 step, same box
+// (profiles/r5ar/). GHOSTM_K1_PREVALL=0 builds the lane-0 load and DPP (A/B)
+#ifndef GHOSTM_K1_PREVALL
+#define GHOSTM_K1_PREVALL 1
+#endif
+// Pass 2: queue slots by v_mbcnt_lo/hi from the ballot, each lane's keep bit
+// kept from the test (GHOSTM_K1_MBCNT=0: 64-bit masks and popcounts, A/B)
+#ifndef GHOSTM_K1_MBCNT
+#define GHOSTM_K1_MBCNT 0
+#endif
+// Pass 2 (A/B): the filter test without branches
+#ifndef GHOSTM_K1_P2BF
+#define GHOSTM_K1_P2BF 0
+#endif
 #ifndef GHOSTM_K1_GUARD  // A/B: 1 skips the wave's chunk slots past n by scalar branches
 #define GHOSTM_K1_GUARD 0    // (measured slower: 13.42 against 13.14 ms per class-1 launch)
 #endif
@@ -732,7 +775,9 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   constexpr uint32_t kChunks = KE * kW;
   constexpr uint32_t kNone = 0xFFFFFFFFu;
   static_assert((FSLOTS & (FSLOTS - 1)) == 0 && TSLOTS * 2 >= QCAP * 3 && TSLOTS % BLOCK == 0, "filter shape");
-  __shared__ uint32_t s_delta[kMaxLists];     // list j: position index of entry i = i + s_delta[j]
+  // list j: position index of entry i = i + delta(j); PREVALL keeps (delta,
+  // s_off, the list's diagonal origin j * shift) per list, one 128-bit read per entry
+  __shared__ __attribute__((aligned(16))) uint32_t s_delta[GHOSTM_K1_PREVALL ? 4 * kMaxLists : kMaxLists];
   __shared__ uint32_t s_off[kMaxLists + 1];
   __shared__ uint8_t s_cfirst[kChunks];
   __shared__ __attribute__((aligned(16))) uint32_t s_emit[kMaxSlotCap];
@@ -757,7 +802,11 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   const uint32_t excl = BlockExclusiveScan(len, s_part, &s_total);
   if (tid < nl) {
     s_off[tid] = excl;
-    s_delta[tid] = beg - excl;
+    if constexpr (GHOSTM_K1_PREVALL) {
+      reinterpret_cast<uint4 *>(s_delta)[tid] = make_uint4(beg - excl, excl, tid * a.shift, 0u);
+    } else {
+      s_delta[tid] = beg - excl;
+    }
     for (uint32_t c = (excl + 63) >> 6; (c << 6) < excl + len && c < kChunks; ++c) s_cfirst[c] = (uint8_t)tid;
   }
   if (tid == 0) s_off[nl] = s_total;
@@ -791,6 +840,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   const uint32_t ne =
       GHOSTM_K1_GUARD ? __builtin_amdgcn_readfirstlane(nch > wave ? min(KE, (nch - wave + kW - 1) / kW) : 0u) : KE;
 #if GHOSTM_K1_PREFETCH  // A/B variant (tools/altlib.sh -DGHOSTM_K1_PREFETCH=1)
+  static_assert(!GHOSTM_K1_PREVALL, "PREFETCH reads the plain delta table");
   // every chunk's positions are requested before any is used (one exposure of
   // the gather latency per wave instead of one per four chunks)
   uint32_t pos[KE], prv[KE], lst[KE];
@@ -880,7 +930,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
       for (uint32_t u = 0; u < 4; ++u) bin[e0 + u] = kNone;
       continue;
     }
-    uint32_t pos[4], prv[4], lst[4], ii[4], jj[4], dd[4];
+    uint32_t pos[4], prv[4], lst[4], ii[4], jj[4], dd[4], lo[4], og[4];
     // the four entries' list bytes, then their position offsets, as two batches
     // of LDS reads (every entry index stays inside the byte table)
 #pragma unroll
@@ -889,12 +939,64 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
       jj[u] = s_lst[ii[u]];
     }
 #pragma unroll
-    for (uint32_t u = 0; u < 4; ++u) dd[u] = s_delta[jj[u]];
+    for (uint32_t u = 0; u < 4; ++u) {
+      if constexpr (GHOSTM_K1_PREVALL) {
+        const uint4 v = reinterpret_cast<const uint4 *>(s_delta)[jj[u]];
+        dd[u] = v.x;
+        lo[u] = v.y;
+        og[u] = v.z;
+      } else {
+        dd[u] = s_delta[jj[u]];
+        lo[u] = 0;
+        og[u] = 0;
+      }
+    }
     // (kept here: the compiler otherwise sinks both reads into each entry's
     // branch below and waits for them one entry at a time)
 #pragma unroll
-    for (uint32_t u = 0; u < 4; ++u) asm volatile("" : "+v"(dd[u]));
-#if GHOSTM_K1_BATCH
+    for (uint32_t u = 0; u < 4; ++u) {
+      if constexpr (!GHOSTM_K1_PREVALL) asm volatile("" : "+v"(dd[u]));  // (PREVALL: no branches)
+    }
+#if GHOSTM_K1_PREVALL
+    // every lane loads its entry's list predecessor (the same lines as the
+    // entries, no lane-0 branch, no DPP): an entry past n or first in its list
+    // has none; its load is out of the buffer's range (returns 0, no access)
+    const __amdgpu_buffer_rsrc_t pr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)a.positions, 0, 0x7FFFFFFF, 0x00020000);
+    // an entry past n has list 0 (its list byte): it reads inside the positions'
+    // tail pad (kPosTailPad >= the entry slots), and its bin is dropped
+    static_assert(64 * KE * kW <= kPosTailPad, "entry slots past n stay inside the positions' tail pad");
+    bool hp[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) {
+      const uint32_t at = ii[u] + dd[u];
+      hp[u] = ii[u] != lo[u];  // the entry has a list predecessor (at >= 1)
+      pos[u] = __builtin_amdgcn_raw_buffer_load_b32(pr, at * 4, 0, 0);
+      prv[u] = __builtin_amdgcn_raw_buffer_load_b32(pr, hp[u] ? at * 4 - 4 : 0x80000000u, 0, 0);
+    }
+    uint32_t fw[4], fb[4], old[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) {
+      const uint32_t d0 = og[u];
+      const uint32_t b = (pos[u] - d0) >> a.log_region;
+      const bool dup = hp[u] && ((prv[u] - d0) >> a.log_region) == b;
+      const bool live = ii[u] < n && !dup;
+      const uint32_t x = live ? b : kNone;
+      bin[e0 + u] = x;
+      const uint32_t cell = x & (FSLOTS - 1);
+      fw[u] = live ? cell >> 4 : lane;
+      fb[u] = live ? 1u << ((cell & 15) * 2) : 0u;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) old[u] = atomicOr(&s_flt[fw[u]], fb[u]);
+    // the seen-twice marks without a branch (an entry seen once ORs 0)
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) {
+      atomicOr(&s_flt[fw[u]], (old[u] & fb[u]) << 1);
+      if (GHOSTM_K1_READ2 && fb[u] && fw[u] == 0 && fb[u] < 16u)  // cells 0 and 1: the guard copy
+        atomicOr(&s_flt[kFWords], (old[u] & fb[u]) ? fb[u] * 3u : fb[u]);
+    }
+#elif GHOSTM_K1_BATCH
     // positions through a raw buffer (32-bit offsets, no 64-bit address math);
     // entries past n read entry 0's word (any valid one) and are dropped below
     const __amdgpu_buffer_rsrc_t pr =
@@ -994,26 +1096,42 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   };
   uint32_t wave_n = 0;
   unsigned long long bal[KE];  // wave-uniform: SGPR pairs
+  bool keep[KE];               // this lane's bit of bal[e]
 #pragma unroll
   for (uint32_t e = 0; e < KE; ++e) {
     bal[e] = 0;
+    keep[e] = false;
     if (e >= ne) continue;
     const uint32_t x = bin[e];
     bool nd = false;
-    if (x != kNone) nd = x <= 1 || (near(x) & 0x19u) != 0;  // seen(x - 1), twice(x), seen(x + 1)
+    if constexpr (GHOSTM_K1_P2BF) {
+      // branch-free: every lane reads its cells (no bin: cells of kNone, in
+      // range, result dropped), the three tests combined without short circuit
+      const uint32_t nb = near(x);
+      nd = (x != kNone) & ((x <= 1) | ((nb & 0x19u) != 0));
+    } else if (x != kNone) {
+      nd = x <= 1 || (near(x) & 0x19u) != 0;  // seen(x - 1), twice(x), seen(x + 1)
+    }
     bal[e] = __ballot(nd);
+    keep[e] = nd;
     wave_n += (uint32_t)__popcll(bal[e]);
   }
   uint32_t qbase = 0;
   if (lane == 0) qbase = atomicAdd(&s_qn, wave_n);
-  qbase = (uint32_t)__shfl((int)qbase, 0);
+  qbase = GHOSTM_K1_MBCNT ? __builtin_amdgcn_readfirstlane(qbase) : (uint32_t)__shfl((int)qbase, 0);
 #pragma unroll
   for (uint32_t e = 0; e < KE; ++e) {
     if (e >= ne) continue;
     const unsigned long long m = bal[e];
-    const bool nd = (m >> lane) & 1ull;
-    const uint32_t at = qbase + (uint32_t)__popcll(m & ((1ull << lane) - 1));
-    if (nd && at < QCAP) s_q[at] = bin[e];
+    if constexpr (GHOSTM_K1_MBCNT) {
+      // queue slot: the kept lanes below this one (v_mbcnt_lo/hi) past qbase
+      const uint32_t at = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, qbase));
+      if (keep[e] && at < QCAP) s_q[at] = bin[e];
+    } else {
+      const bool nd = (m >> lane) & 1ull;
+      const uint32_t at = qbase + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+      if (nd && at < QCAP) s_q[at] = bin[e];
+    }
     qbase += (uint32_t)__popcll(m);
   }
   __syncthreads();
