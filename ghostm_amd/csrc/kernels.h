@@ -405,8 +405,7 @@ __device__ inline uint32_t BinHash(uint32_t b) { return b * 2654435761u; }
 // the quarter-rate v_mul_lo_u32 / v_mul_hi_u32 pair: h = b * C (low 32 bits),
 // bucket = ((h >> s) * buckets) >> (32 - s) with 2^s >= buckets, so the product
 // stays below 2^32. Bins are < 2^22 (kHashBinLimit + 1). Any hash gives the same
-// counts and output (the table only has to find its keys); GHOSTM_K1_HASH24=0
-// keeps the 32-bit multiplicative hash (A/B)
+// counts and output (the table only has to find its keys). A/B: GHOSTM_K1_HASH24=1
 #ifndef GHOSTM_K1_HASH24
 #define GHOSTM_K1_HASH24 0
 #endif
@@ -697,8 +696,9 @@ __host__ __device__ constexpr uint32_t FilterWords(uint32_t fslots) { return fsl
 #ifndef GHOSTM_K1_PREVALL
 #define GHOSTM_K1_PREVALL 1
 #endif
-// Pass 2: queue slots by v_mbcnt_lo/hi from the ballot, each lane's keep bit
-// kept from the test (GHOSTM_K1_MBCNT=0: 64-bit masks and popcounts, A/B)
+// Pass 2 (A/B, GHOSTM_K1_MBCNT=1): queue slots by v_mbcnt_lo/hi from the
+// ballot, each lane's keep bit kept from the test, instead of 64-bit lane masks
+// and popcounts
 #ifndef GHOSTM_K1_MBCNT
 #define GHOSTM_K1_MBCNT 0
 #endif
