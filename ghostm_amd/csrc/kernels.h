@@ -405,9 +405,10 @@ __device__ inline uint32_t BinHash(uint32_t b) { return b * 2654435761u; }
 // the quarter-rate v_mul_lo_u32 / v_mul_hi_u32 pair: h = b * C (low 32 bits),
 // bucket = ((h >> s) * buckets) >> (32 - s) with 2^s >= buckets, so the product
 // stays below 2^32. Bins are < 2^22 (kHashBinLimit + 1). Any hash gives the same
-// counts and output (the table only has to find its keys). A/B: GHOSTM_K1_HASH24=1
+// counts and output (the table only has to find its keys). GHOSTM_K1_HASH24=0
+// keeps the 32-bit multiplicative hash (A/B)
 #ifndef GHOSTM_K1_HASH24
-#define GHOSTM_K1_HASH24 0
+#define GHOSTM_K1_HASH24 1
 #endif
 __host__ __device__ constexpr uint32_t CeilLog2(uint32_t v) {
   uint32_t l = 0;
@@ -434,8 +435,8 @@ struct BinTable {
     if constexpr (GHOSTM_K1_HASH24) {
       constexpr uint32_t kS = CeilLog2(kBuckets);
       static_assert(kS >= 8 && kS < 24, "(h >> s) and the bucket count fit 24 bits");
-      const uint32_t h = __umul24(b, 0x9E3779u);
-      return __umul24(h >> kS, kBuckets) >> (32 - kS);
+      const uint32_t h = (uint32_t)__umul24(b, 0x9E3779u);
+      return (uint32_t)__umul24(h >> kS, kBuckets) >> (32 - kS);  // (__umul24 is int-typed: shift unsigned)
     } else {
       return __umulhi(BinHash(b), kBuckets);
     }
@@ -696,11 +697,12 @@ __host__ __device__ constexpr uint32_t FilterWords(uint32_t fslots) { return fsl
 #ifndef GHOSTM_K1_PREVALL
 #define GHOSTM_K1_PREVALL 1
 #endif
-// Pass 2 (A/B, GHOSTM_K1_MBCNT=1): queue slots by v_mbcnt_lo/hi from the
-// ballot, each lane's keep bit kept from the test, instead of 64-bit lane masks
-// and popcounts
+// Pass 2: queue slots by v_mbcnt_lo/hi from the ballot, each lane's keep bit
+// kept from the test, instead of 64-bit lane masks and popcounts (with HASH24:
+// class-1 filter 10.35 -> 10.15 ms, K1 24.5-24.7 -> 24.1-24.2 ms per cfg4 step,
+// profiles/r5av/). GHOSTM_K1_MBCNT=0 keeps the masks (A/B)
 #ifndef GHOSTM_K1_MBCNT
-#define GHOSTM_K1_MBCNT 0
+#define GHOSTM_K1_MBCNT 1
 #endif
 // Pass 2 (A/B): the filter test without branches
 #ifndef GHOSTM_K1_P2BF
