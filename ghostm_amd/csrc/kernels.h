@@ -697,6 +697,10 @@ __host__ __device__ constexpr uint32_t FilterWords(uint32_t fslots) { return fsl
 #ifndef GHOSTM_K1_PREVALL
 #define GHOSTM_K1_PREVALL 1
 #endif
+// (A/B: the classes with at least this many threads use it)
+#ifndef GHOSTM_K1_PREVALL_MIN_BLOCK
+#define GHOSTM_K1_PREVALL_MIN_BLOCK 256
+#endif
 // Pass 2: queue slots by v_mbcnt_lo/hi from the ballot, each lane's keep bit
 // kept from the test, instead of 64-bit lane masks and popcounts (with HASH24:
 // class-1 filter 10.35 -> 10.15 ms, K1 24.5-24.7 -> 24.1-24.2 ms per cfg4 step,
@@ -779,7 +783,8 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   static_assert((FSLOTS & (FSLOTS - 1)) == 0 && TSLOTS * 2 >= QCAP * 3 && TSLOTS % BLOCK == 0, "filter shape");
   // list j: position index of entry i = i + delta(j); PREVALL keeps (delta,
   // s_off, the list's diagonal origin j * shift) per list, one 128-bit read per entry
-  __shared__ __attribute__((aligned(16))) uint32_t s_delta[GHOSTM_K1_PREVALL ? 4 * kMaxLists : kMaxLists];
+  constexpr bool kPrevAll = GHOSTM_K1_PREVALL && BLOCK >= GHOSTM_K1_PREVALL_MIN_BLOCK;
+  __shared__ __attribute__((aligned(16))) uint32_t s_delta[kPrevAll ? 4 * kMaxLists : kMaxLists];
   __shared__ uint32_t s_off[kMaxLists + 1];
   __shared__ uint8_t s_cfirst[kChunks];
   __shared__ __attribute__((aligned(16))) uint32_t s_emit[kMaxSlotCap];
@@ -804,7 +809,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   const uint32_t excl = BlockExclusiveScan(len, s_part, &s_total);
   if (tid < nl) {
     s_off[tid] = excl;
-    if constexpr (GHOSTM_K1_PREVALL) {
+    if constexpr (kPrevAll) {
       reinterpret_cast<uint4 *>(s_delta)[tid] = make_uint4(beg - excl, excl, tid * a.shift, 0u);
     } else {
       s_delta[tid] = beg - excl;
@@ -842,7 +847,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   const uint32_t ne =
       GHOSTM_K1_GUARD ? __builtin_amdgcn_readfirstlane(nch > wave ? min(KE, (nch - wave + kW - 1) / kW) : 0u) : KE;
 #if GHOSTM_K1_PREFETCH  // A/B variant (tools/altlib.sh -DGHOSTM_K1_PREFETCH=1)
-  static_assert(!GHOSTM_K1_PREVALL, "PREFETCH reads the plain delta table");
+  static_assert(!kPrevAll, "PREFETCH reads the plain delta table");
   // every chunk's positions are requested before any is used (one exposure of
   // the gather latency per wave instead of one per four chunks)
   uint32_t pos[KE], prv[KE], lst[KE];
@@ -942,7 +947,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
     }
 #pragma unroll
     for (uint32_t u = 0; u < 4; ++u) {
-      if constexpr (GHOSTM_K1_PREVALL) {
+      if constexpr (kPrevAll) {
         const uint4 v = reinterpret_cast<const uint4 *>(s_delta)[jj[u]];
         dd[u] = v.x;
         lo[u] = v.y;
@@ -957,9 +962,9 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
     // branch below and waits for them one entry at a time)
 #pragma unroll
     for (uint32_t u = 0; u < 4; ++u) {
-      if constexpr (!GHOSTM_K1_PREVALL) asm volatile("" : "+v"(dd[u]));  // (PREVALL: no branches)
+      if constexpr (!kPrevAll) asm volatile("" : "+v"(dd[u]));  // (PREVALL: no branches)
     }
-#if GHOSTM_K1_PREVALL
+    if constexpr (kPrevAll) {
     // every lane loads its entry's list predecessor (the same lines as the
     // entries, no lane-0 branch, no DPP): an entry past n or first in its list
     // has none; its load is out of the buffer's range (returns 0, no access)
@@ -998,7 +1003,8 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
       if (GHOSTM_K1_READ2 && fb[u] && fw[u] == 0 && fb[u] < 16u)  // cells 0 and 1: the guard copy
         atomicOr(&s_flt[kFWords], (old[u] & fb[u]) ? fb[u] * 3u : fb[u]);
     }
-#elif GHOSTM_K1_BATCH
+    } else {
+#if GHOSTM_K1_BATCH
     // positions through a raw buffer (32-bit offsets, no 64-bit address math);
     // entries past n read entry 0's word (any valid one) and are dropped below
     const __amdgpu_buffer_rsrc_t pr =
@@ -1076,6 +1082,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
       bin[e0 + u] = x;
     }
 #endif
+    }
   }
 #endif
   __syncthreads();
