@@ -531,6 +531,20 @@ Session::Session(const AlignerOptions &opt, uint32_t shard_rank, uint32_t shard_
     : opt_(opt) {
   threads_ = HostThreads();
   if (shard_world == 0 || shard_rank >= shard_world) throw std::invalid_argument("shard rank outside the world");
+  try {
+    Create(shard_rank, shard_world, ex);
+  } catch (...) {
+    // a throwing constructor runs no destructor: free the resident chunks here
+    DeviceModule &dev = DeviceModule::Get();
+    for (QueryData &q : queries_) dev.Free(q.dev);
+    for (DbData &d : dbs_) dev.Free(d.dev);
+    queries_.clear();
+    dbs_.clear();
+    throw;
+  }
+}
+
+void Session::Create(uint32_t shard_rank, uint32_t shard_world, const ShardExchange *ex) {
   shard_world_ = shard_world;
   const bool local = shard_world > 1 && ex && ex->fn;  // rank-local reads + exchange
   std::vector<uint32_t> chunk_nseq;
@@ -645,6 +659,20 @@ void Session::Load(uint32_t shard_rank, uint32_t shard_world, bool local, std::v
   std::vector<QueryChunkIndex> qidx(local ? nq_chunks : 0);
   std::vector<DbData> dread(nd_chunks);
   std::vector<char> qok(nq_chunks, 0), dok(nd_chunks, 0);
+  // chunks uploaded here but not (yet) handed to queries_/dbs_ are freed on every
+  // exit, the error exits included (a chunk handed over has its handle nulled
+  // here; the constructor frees queries_/dbs_ if creation fails later)
+  struct Unadopted {
+    std::vector<QueryData> &q;
+    std::vector<DbData> &d;
+    ~Unadopted() {
+      DeviceModule &m = DeviceModule::Get();
+      for (QueryData &x : q)
+        if (x.dev) m.Free(x.dev);
+      for (DbData &x : d)
+        if (x.dev) m.Free(x.dev);
+    }
+  } unadopted{qread, dread};
   // (each query chunk's name groups and WriteOutput lengths are derived on its
   // reading thread too; a rank-local shard only indexes the query chunks here).
   // A DB chunk is uploaded by its reading thread as soon as it is read, one
@@ -710,9 +738,9 @@ void Session::Load(uint32_t shard_rank, uint32_t shard_world, bool local, std::v
     dread[nd_kept].global_base = dbase;
     dbase += dread[nd_kept].chunk.nseq;
     dbs_.push_back(std::move(dread[nd_kept]));
+    dread[nd_kept].dev = nullptr;
   }
-  for (uint32_t k = nd_kept; k < nd_chunks; ++k)  // read past a missing chunk: not used
-    if (dread[k].dev) dev.Free(dread[k].dev);
+  // chunks read past a missing one are not used (freed by `unadopted`)
   if (dbs_.empty()) throw std::runtime_error("[Aligner] error: don't find db file.");
   TraceMark("db_read", dbs_.size());
   {
@@ -769,13 +797,17 @@ void Session::Load(uint32_t shard_rank, uint32_t shard_world, bool local, std::v
       for (uint32_t k : read) chunks.push_back(&qread[k]);
       QueryLengths(chunks);
     }
-    for (uint32_t k : read) queries_.push_back(std::move(qread[k]));
+    for (uint32_t k : read) {
+      queries_.push_back(std::move(qread[k]));
+      qread[k].dev = nullptr;
+    }
     TraceMark("slices_read", queries_.size());
   } else {
     for (uint32_t k = 0; k < nchunks; ++k) {
       qread[k].global_base = base;
       base += qread[k].chunk.nseq;
       queries_.push_back(std::move(qread[k]));
+      qread[k].dev = nullptr;
     }
     if (shard_world > 1) ApplyShard(shard_rank, shard_world);  // may leave no queries
   }
@@ -784,8 +816,7 @@ void Session::Load(uint32_t shard_rank, uint32_t shard_world, bool local, std::v
     if (!q.dev) upload_query(q);  // (uploaded while reading when unsharded)
     q.chunk.seq.Release();  // resident on the device (qlen and names stay on the host)
   }
-  for (uint32_t k = nchunks; k < nq_chunks; ++k)  // read past a missing chunk: not used
-    if (qread[k].dev) dev.Free(qread[k].dev);
+  // query chunks read past a missing one are not used (freed by `unadopted`)
 }
 
 namespace {
@@ -1562,6 +1593,8 @@ void Session::Run(bool stream_to_file) {
   stats_.seed_queries_wide = dt.seed_queries_wide;
   stats_.seed_runs_filter = dt.seed_launches_filter;
   stats_.seed_filter_overflows = dt.seed_filter_overflows;
+  stats_.seed_table_full = dt.seed_table_full;
+  stats_.seed_compact_redo = dt.seed_compact_redo;
   stats_.score_launches_swar = dt.score_launches_swar;
   stats_.score_launches_unit = dt.score_launches_unit;
   stats_.score_launches_pair = dt.score_launches_pair;

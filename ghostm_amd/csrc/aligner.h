@@ -181,6 +181,7 @@ class Session {
   void ApplyShard(uint32_t rank, uint32_t world);
   // shard sessions: the batch plan of every (query chunk, DB chunk)
   void PlanFromCounts(QueryData &q, size_t di, const std::vector<uint32_t> &chunk_counts, uint32_t n);
+  void Create(uint32_t shard_rank, uint32_t shard_world, const ShardExchange *ex);
   void Load(uint32_t shard_rank, uint32_t shard_world, bool local, std::vector<uint32_t> *chunk_nseq,
             std::vector<std::vector<uint64_t>> *rank_lo);
   void AgreeOnCreate(uint32_t rank, uint32_t world, const ShardExchange &ex, const std::string &err,

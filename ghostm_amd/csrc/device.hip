@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <climits>
 #include <cstdio>
 #include <cstdlib>
@@ -51,7 +52,9 @@ struct PinnedBuf {
 // profiles/r5f/cfg3_e2e_trace.log). A block is cached after a device
 // synchronisation, as hipFree would do; a request takes the smallest cached block
 // of 1-2x its size. At most GHOSTM_DEV_POOL_MB (default 8192) stay cached; 0
-// turns the cache off.
+// turns the cache off. The cache never costs an allocation: a hipMalloc that
+// runs out of memory empties it and tries once more (DevBuf::Reserve), and a
+// caller sharing the device (torch, RCCL) can empty it (GhostmDevicePoolTrim).
 class DevPool {
  public:
   static DevPool &Get() {
@@ -87,6 +90,42 @@ class DevPool {
     blocks_.push_back(Block{p, bytes, dev});
     cached_ += bytes;
   }
+  // frees every cached block; returns the bytes freed
+  size_t Trim() {
+    std::lock_guard<std::mutex> lock(mu_);
+    size_t freed = 0;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (const Block &b : blocks_) {
+      (void)hipSetDevice(b.dev);
+      (void)hipFree(b.p);
+      freed += b.bytes;
+    }
+    (void)hipSetDevice(cur);
+    blocks_.clear();
+    cached_ = 0;
+    return freed;
+  }
+  // hipMalloc through the cache's out-of-memory rule: on failure, empty the cache
+  // and try once more. GHOSTM_DEV_OOM_TEST=1 (tests) makes the first attempt fail
+  // whenever blocks are cached, so the retry path runs on any data set.
+  hipError_t Malloc(void **p, size_t bytes) {
+    const char *t = getenv("GHOSTM_DEV_OOM_TEST");
+    hipError_t err = (t && *t == '1' && Cached()) ? hipErrorOutOfMemory : hipMalloc(p, bytes);
+    if (err == hipErrorOutOfMemory && Cached()) {
+      (void)hipGetLastError();  // clear the failed call's error state
+      Trim();
+      ++oom_retries_;
+      err = hipMalloc(p, bytes);
+    }
+    if (err != hipSuccess) *p = nullptr;
+    return err;
+  }
+  size_t Cached() {
+    std::lock_guard<std::mutex> lock(mu_);
+    return cached_;
+  }
+  uint64_t OomRetries() const { return oom_retries_.load(); }
 
  private:
   DevPool() {
@@ -101,6 +140,7 @@ class DevPool {
   std::mutex mu_;
   std::vector<Block> blocks_;
   size_t cached_ = 0, cap_ = 0;
+  std::atomic<uint64_t> oom_retries_{0};
 };
 
 struct DevBuf {
@@ -114,7 +154,7 @@ struct DevBuf {
       if (TraceOn()) TraceMark("dev_reuse", want);
     } else {
       if (TraceOn()) TraceMark("dev_alloc", want);
-      HIP_CHECK(hipMalloc(&p, want));
+      HIP_CHECK(DevPool::Get().Malloc(&p, want));
     }
     bytes = want;
   }
@@ -778,6 +818,8 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
   a.counts = I.counts.as<uint32_t>();
   a.slots = I.slots.as<uint32_t>();
   a.slot_cap = slot_cap;
+  a.probe_windows = 0xFFFFFFFFu;  // BinTable's own bound
+  if (const char *e = getenv("GHOSTM_K1_PROBE_WINDOWS")) a.probe_windows = (uint32_t)strtoul(e, nullptr, 10);
   // the class that held most queries last time is launched now, over every
   // query (its blocks pick their queries from the device bin counts), so the
   // GPU works through it while the host sorts the rest into class lists
@@ -879,7 +921,10 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
   // the host offsets, A/B)
   const char *devoff_env = getenv("GHOSTM_K1_DEVOFF");
   const bool dev_off = !(devoff_env && strcmp(devoff_env, "0") == 0);
-  const uint64_t cand_cap = std::min(I.cand_start.bytes, I.cand_qid.bytes) / 4;
+  // (GHOSTM_K1_CAND_CAP, tests: the device compaction sees at most that many
+  // candidates of room, so its partial-write guard and the host's re-run run)
+  uint64_t cand_cap = std::min(I.cand_start.bytes, I.cand_qid.bytes) / 4;
+  if (const char *e = getenv("GHOSTM_K1_CAND_CAP")) cand_cap = std::min<uint64_t>(cand_cap, strtoull(e, nullptr, 10));
   auto launch_compact = [&](uint64_t cap) {
     hipLaunchKernelGGL(kern::k_compact, dim3((nq + 3) / 4), dim3(256), 0, S(stream_),
                        I.slots.as<uint32_t>(), slot_cap, I.counts.as<uint32_t>(), (const uint8_t *)nullptr,
@@ -934,28 +979,34 @@ uint64_t DeviceModule::Seed(DevQuery *q, DevDb *d, const SeedConfig &cfg,
   count_pass(pinned ? I.h_counts.as<uint32_t>() : counts->data());
   bool overflow = false;
   for (uint8_t o : part_over) overflow |= o != 0;
-  if (filter && overflow) {
-    // queries whose filtered queue overflowed: the unfiltered table redoes them
-    std::vector<uint32_t> redo[3];
-    for (int c = 0; c < 3; ++c)
-      for (uint32_t qi : cls[c])
-        if ((*counts)[qi] == kern::kOverflow) redo[c].push_back(qi);
-    if (!redo[0].empty() || !redo[1].empty() || !redo[2].empty()) {
+  if (hash && overflow) {
+    // queries a class-0..2 kernel marked kOverflow: a filtered queue that
+    // overflowed (or a filter table that found no free slot) is redone by the
+    // unfiltered table (k_seed_hash); a table that found no free slot within its
+    // probe bound (BinTable) is redone by the LDS merge kernel (k_seed), which
+    // has no table. Each stage reads the counts back before the next.
+    for (int stage = filter ? 0 : 1; stage < 2; ++stage) {
+      std::vector<uint32_t> redo[3];
+      for (int c = 0; c < 3; ++c)
+        for (uint32_t qi : cls[c])
+          if ((*counts)[qi] == kern::kOverflow) redo[c].push_back(qi);
       std::vector<uint32_t> all(redo[0]);
       all.insert(all.end(), redo[1].begin(), redo[1].end());
       all.insert(all.end(), redo[2].begin(), redo[2].end());
+      if (all.empty()) break;
       I.qlist.Reserve(all.size() * 4);
       HIP_CHECK(hipMemcpyAsync(I.qlist.p, all.data(), all.size() * 4, hipMemcpyHostToDevice, S(stream_)));
       size_t at = 0;
       for (int c = 0; c < 3; ++c) {
         kern::SeedArgs b = a;
         b.query_list = I.qlist.as<uint32_t>() + at;
-        LaunchSeedHashClass(c, b, (uint32_t)redo[c].size(), S(stream_));
+        if (stage == 0) LaunchSeedHashClass(c, b, (uint32_t)redo[c].size(), S(stream_));
+        else LaunchSeedClass(c, b, (uint32_t)redo[c].size(), S(stream_));
         at += redo[c].size();
       }
       HIP_CHECK(hipMemcpyAsync(counts->data(), I.counts.p, (size_t)nq * 4, hipMemcpyDeviceToHost, S(stream_)));
       HIP_CHECK(hipStreamSynchronize(S(stream_)));
-      times_.seed_filter_overflows += all.size();
+      (stage == 0 ? times_.seed_filter_overflows : times_.seed_table_full) += all.size();
       count_pass(counts->data());
     }
   }
@@ -1900,13 +1951,21 @@ void DeviceModule::TraceBack(DevQuery *q, DevDb *d, uint32_t n, const uint32_t *
   }
 }
 
+const char *SourceHash();  // build_hash.cpp, generated by the Makefile (ghostm_amd/srchash.py)
+
 const char *DeviceBuildInfo() {
-  return "ghostm_hip gfx950: K1 k_seed_lists/k_seed_filter/k_seed_hash/k_seed, K2 k_score16f/k_score16/k_score, "
-         "K3 k_tb_scan/k_traceback_key/k_traceback, K4 k_merge_wave/k_merge"
+  static const std::string info =
+      std::string("ghostm_hip gfx950: K1 k_seed_lists/k_seed_filter/k_seed_hash/k_seed, K2 k_score16f/k_score16/"
+                  "k_score, K3 k_tb_scan/k_traceback_key/k_traceback, K4 k_merge_wave/k_merge"
 #ifdef GHOSTM_LDS_POISON
-         "; LDS poison build"
+                  "; LDS poison build"
 #endif
-      ;
+#ifdef GHOSTM_ALT_TAG
+                  "; A/B build " GHOSTM_ALT_TAG
+#endif
+                  ) +
+      "; src " + SourceHash();
+  return info.c_str();
 }
 
 // ============================================================ reference C ABI
@@ -1945,6 +2004,14 @@ extern "C" {
 const char *GhostmGetLastError(void) { return g_last_error.c_str(); }
 
 const char *GhostmBuildInfo(void) { return DeviceBuildInfo(); }
+
+uint64_t GhostmDevicePoolTrim(void) { return DevPool::Get().Trim(); }
+
+int GhostmDevicePoolInfo(uint64_t *cached_bytes, uint64_t *oom_retries) {
+  if (cached_bytes) *cached_bytes = DevPool::Get().Cached();
+  if (oom_retries) *oom_retries = DevPool::Get().OomRetries();
+  return 0;
+}
 
 int InitGpu(void) {
   RefState &r = Ref();

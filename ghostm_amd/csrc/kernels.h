@@ -168,6 +168,7 @@ struct SeedArgs {
   // class launched before the host has read the bin counts), else returns
   const uint32_t *nbins;
   uint32_t nb_lo, nb_hi;
+  uint32_t probe_windows;         // bin table probe bound (BinTable::Bound); tests lower it
 };
 
 // The query a K1b block serves, or kNoQuery (block-uniform: return at once).
@@ -400,22 +401,14 @@ __global__ __launch_bounds__(BLOCK) void k_seed(SeedArgs a) {
 //     written in ascending order. Same output as k_seed in slot mode; queries
 //     with more candidates only get their count here and are redone by k_seed in
 //     offset mode. Needs every bin + 2 < 2^21 (kHashBinLimit).
-__device__ inline uint32_t BinHash(uint32_t b) { return b * 2654435761u; }
 // HASH24: the bucket from full-rate 24-bit multiplies (v_mul_u32_u24) instead of
-// the quarter-rate v_mul_lo_u32 / v_mul_hi_u32 pair: h = b * C (low 32 bits),
-// bucket = ((h >> s) * buckets) >> (32 - s) with 2^s >= buckets, so the product
-// stays below 2^32. Bins are < 2^22 (kHashBinLimit + 1). Any hash gives the same
-// counts and output (the table only has to find its keys). GHOSTM_K1_HASH24=0
-// keeps the 32-bit multiplicative hash (A/B)
+// the quarter-rate v_mul_lo_u32 / v_mul_hi_u32 pair (BinBucket, seed_lists.h;
+// every bucket < kBuckets is checked on the host, tests/test_seed_lists.py). Any
+// hash gives the same counts and output (the table only has to find its keys).
+// GHOSTM_K1_HASH24=0 keeps the 32-bit multiplicative hash (A/B)
 #ifndef GHOSTM_K1_HASH24
 #define GHOSTM_K1_HASH24 1
 #endif
-__host__ __device__ constexpr uint32_t CeilLog2(uint32_t v) {
-  uint32_t l = 0;
-  while ((1u << l) < v) ++l;
-  return l;
-}
-constexpr uint32_t kHashBinLimit = 1u << 21;
 
 // Slot word: (bin + 1) << 11 | count << 3, low three bits zero; 0 = empty.
 // Linear probing over slots, read eight at a time: a window is two 4-slot
@@ -431,16 +424,7 @@ struct BinTable {
   static constexpr uint32_t kBuckets = TSLOTS / 4;
   uint32_t *tab;
   __device__ static uint32_t Key(uint32_t b) { return (b + 1) << 11; }
-  __device__ static uint32_t Bucket(uint32_t b) {
-    if constexpr (GHOSTM_K1_HASH24) {
-      constexpr uint32_t kS = CeilLog2(kBuckets);
-      static_assert(kS >= 8 && kS < 24, "(h >> s) and the bucket count fit 24 bits");
-      const uint32_t h = (uint32_t)__umul24(b, 0x9E3779u);
-      return (uint32_t)__umul24(h >> kS, kBuckets) >> (32 - kS);  // (__umul24 is int-typed: shift unsigned)
-    } else {
-      return __umulhi(BinHash(b), kBuckets);
-    }
-  }
+  __device__ static uint32_t Bucket(uint32_t b) { return BinBucket<kBuckets, GHOSTM_K1_HASH24 != 0>(b); }
   __device__ static uint32_t Next(uint32_t k) { return k + 1 == kBuckets ? 0u : k + 1; }
   __device__ static uint32_t Min8(const uint32_t v[8]) {
     return min(min(min(v[0], v[1]), v[2]), min(min(min(v[3], v[4]), v[5]), min(v[6], v[7])));
@@ -467,10 +451,22 @@ struct BinTable {
     for (int m = 0; m < 8; ++m) u[m] = sl[m] + (uint32_t)m;
     return Min8(u);
   }
+  // Probe bound: (kBuckets + 1) / 2 windows visit every bucket, so a bin that
+  // is in the table is found and an absent one meets an empty slot (load <= 2/3)
+  // well inside it. The bound is what a wrong bucket or a full table costs: an
+  // Insert past it returns kFull and the kernel marks the query kOverflow (the
+  // host redoes it with a table-free kernel) instead of probing forever. A
+  // Count past it returns 0, which is exact whenever no Insert returned kFull.
+  // `windows` = min(SeedArgs::probe_windows, kMaxWindows): tests lower it
+  // (GHOSTM_K1_PROBE_WINDOWS) to drive queries into the redo.
+  static constexpr uint32_t kMaxWindows = (kBuckets + 1) / 2;
+  static constexpr uint32_t kFull = 0xFFFFFFFEu;
+  uint32_t windows;
+  __device__ static uint32_t Bound(uint32_t w) { return w < kMaxWindows ? w : kMaxWindows; }
   __device__ uint32_t Count(uint32_t b) const {
     const uint32_t key = Key(b);
     uint32_t k = Bucket(b);
-    while (true) {
+    for (uint32_t w = 0; w < windows; ++w) {
       uint32_t sl[8], k1;
       Window(k, sl, &k1);
       const uint32_t mt = Match(sl, key);
@@ -478,15 +474,18 @@ struct BinTable {
       if (Min8(sl) == 0) return 0;
       k = Next(k1);
     }
+    return 0;
   }
   __device__ uint32_t *Slot(uint32_t k, uint32_t k1, uint32_t m) const {
     return tab + (m < 4 ? k * 4 + m : k1 * 4 + (m - 4));
   }
-  // returns the slot index when this call created the bin's slot, else ~0u
+  // returns the slot index when this call created the bin's slot, ~0u when the
+  // bin was there, kFull when no window within the bound had room
   __device__ uint32_t Insert(uint32_t b) {
     const uint32_t key = Key(b);
     uint32_t k = Bucket(b);
-    while (true) {
+    uint32_t w = 0;
+    while (w < windows) {
       uint32_t sl[8], k1;
       Window(k, sl, &k1);
       const uint32_t mt = Match(sl, key);
@@ -497,6 +496,7 @@ struct BinTable {
       const uint32_t e = Empty(sl);
       if (e >= 8) {
         k = Next(k1);
+        ++w;
         continue;
       }
       uint32_t *slot = Slot(k, k1, e);
@@ -506,8 +506,10 @@ struct BinTable {
         atomicAdd(slot, 8u);
         return ~0u;
       }
-      // another bin took the slot first: look at the same window again
+      // another bin took the slot first: look at the same window again (each
+      // retry follows a slot being filled, so at most eight per window)
     }
+    return kFull;
   }
 };
 
@@ -548,7 +550,7 @@ template <uint32_t BLOCK, uint32_t TSLOTS>
 __device__ __forceinline__ void EmitFromTable(const SeedArgs &a, uint32_t q, uint32_t *s_tab, uint32_t *s_emit,
                                               uint32_t *s_part, uint32_t *s_total_p) {
   constexpr uint32_t kPer = TSLOTS / BLOCK;
-  BinTable<TSLOTS> table{s_tab};
+  BinTable<TSLOTS> table{s_tab, BinTable<TSLOTS>::Bound(a.probe_windows)};
   const uint32_t tid = threadIdx.x;
   // 2. emission test per occupied slot (each lane walks only its own occupied
   //    slots); the phantom bin 0 (c(0) = 0, c(1) >= T)
@@ -600,7 +602,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed_hash(SeedArgs a) {
   __shared__ uint8_t s_cfirst[kChunks];      // first list of each 64-entry chunk
   __shared__ __attribute__((aligned(16))) uint32_t s_emit[kMaxSlotCap];
   __shared__ uint32_t s_part[BLOCK / 64];
-  __shared__ uint32_t s_total;
+  __shared__ uint32_t s_total, s_full;
   constexpr uint32_t kPer = TSLOTS / BLOCK;
   static_assert(kPer <= 32 && kPer * BLOCK == TSLOTS && TSLOTS % 8 == 0, "table shape");
   static_assert(kMaxLists <= 256, "list index in a byte");
@@ -611,7 +613,8 @@ __global__ __launch_bounds__(BLOCK) void k_seed_hash(SeedArgs a) {
   const uint32_t nl = a.nlists;
 #pragma unroll
   for (uint32_t k = 0; k < kPer; ++k) s_tab[tid + k * BLOCK] = 0;
-  BinTable<TSLOTS> table{s_tab};
+  if (tid == 0) s_full = 0;  // (ordered before the inserts by the scan's barriers)
+  BinTable<TSLOTS> table{s_tab, BinTable<TSLOTS>::Bound(a.probe_windows)};
 
   // 1. count. The block's lists are concatenated (s_off = prefix of their
   //    lengths) and cut into 64-entry chunks dealt round-robin to the waves,
@@ -664,11 +667,15 @@ __global__ __launch_bounds__(BLOCK) void k_seed_hash(SeedArgs a) {
         const uint32_t d0 = __umul24(j, a.shift);  // j < 128: full-rate 24-bit multiply
         const uint32_t bin = (pos[u] - d0) >> a.log_region;
         const bool dup = prev_pos != 0xFFFFFFFFu && ((prev_pos - d0) >> a.log_region) == bin;
-        if (!dup) table.Insert(bin);
+        if (!dup && table.Insert(bin) == BinTable<TSLOTS>::kFull) s_full = 1;
       }
     }
   }
   __syncthreads();
+  if (s_full) {  // block-uniform: the table-free merge kernel redoes the query
+    if (tid == 0) a.counts[q] = kOverflow;
+    return;
+  }
 
   EmitFromTable<BLOCK, TSLOTS>(a, q, s_tab, s_emit, s_part, &s_total);
 }
@@ -789,7 +796,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   __shared__ uint8_t s_cfirst[kChunks];
   __shared__ __attribute__((aligned(16))) uint32_t s_emit[kMaxSlotCap];
   __shared__ uint32_t s_part[kW];
-  __shared__ uint32_t s_total, s_qn;
+  __shared__ uint32_t s_total, s_qn, s_full;
 
   const uint32_t q = SeedBlockQuery(a);
   if (q == kNoQuery) return;
@@ -800,7 +807,10 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   static_assert(kFWordsPad % 4 == 0 && TSLOTS % 4 == 0, "16-byte zeroing");
   for (uint32_t k = tid; k < (ALIAS ? kFWordsPad : kFWordsPad + TSLOTS) / 4; k += BLOCK)
     reinterpret_cast<uint4 *>(s_dyn)[k] = make_uint4(0u, 0u, 0u, 0u);
-  if (tid == 0) s_qn = 0;
+  if (tid == 0) {
+    s_qn = 0;
+    s_full = 0;
+  }
   uint32_t len = 0, beg = 0;
   if (tid < nl) {
     beg = a.list_beg[(size_t)q * nl + tid];
@@ -1202,14 +1212,19 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   //    bin's slot remembers it, so step 4 visits each occupied slot once with
   //    the queue's density (<= QCAP / BLOCK per lane) instead of walking the
   //    table's TSLOTS / BLOCK slots per lane
-  BinTable<TSLOTS> table{s_tab};
+  BinTable<TSLOTS> table{s_tab, BinTable<TSLOTS>::Bound(a.probe_windows)};
   uint32_t made[kQPer];
 #pragma unroll
   for (uint32_t u = 0; u < kQPer; ++u) {
     const uint32_t k = tid + u * BLOCK;
     made[u] = k < qn ? table.Insert(s_q[k]) : kNone;
+    if (made[u] == BinTable<TSLOTS>::kFull) s_full = 1;
   }
   __syncthreads();
+  if (s_full) {  // block-uniform: redone by k_seed_hash (and by k_seed if that fills too)
+    if (tid == 0) a.counts[q] = kOverflow;
+    return;
+  }
   GHOSTM_K1_PHASE_END(4);
 
   // 4. emission rule per created slot, as EmitFromTable

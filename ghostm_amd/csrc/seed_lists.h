@@ -1,5 +1,6 @@
-// seed_lists.h — K1's entry -> list byte table (k_seed_filter phase 0), shared
-// by the kernel and the host test tests/native/test_seed_lists.cpp.
+// seed_lists.h — K1 arithmetic shared by the kernels and the host tests: the
+// entry -> list byte table (k_seed_filter phase 0, tests/native/test_seed_lists.cpp)
+// and the exact bin table's bucket hash (BinTable, tests/native/test_bin_bucket.cpp).
 #pragma once
 #include <cstdint>
 
@@ -30,6 +31,42 @@ GHOSTM_SEED_HD inline void ListBytes16(uint32_t e0, uint32_t j, const uint32_t *
       const uint32_t c = b > 4 * w ? b - 4 * w : 0u;
       wv[w] += c >= 4 ? 0u : 0x01010101u << (8 * c);
     }
+  }
+}
+
+GHOSTM_SEED_HD constexpr uint32_t CeilLog2(uint32_t v) {
+  uint32_t l = 0;
+  while ((1u << l) < v) ++l;
+  return l;
+}
+
+// v_mul_u32_u24: the low 32 bits of the product of both operands' low 24 bits.
+// (__umul24 is int-typed: its result is cast before any shift.)
+GHOSTM_SEED_HD inline uint32_t Mul24(uint32_t x, uint32_t y) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return (uint32_t)__umul24(x, y);
+#else
+  return (uint32_t)((uint64_t)(x & 0xFFFFFFu) * (uint64_t)(y & 0xFFFFFFu));
+#endif
+}
+
+// K1 bins are < 2^21 (the hash path's limit); BinBucket must hold for every
+// bin <= kHashBinLimit + 1 (the emission also looks up b + 1).
+constexpr uint32_t kHashBinLimit = 1u << 21;
+
+// The bucket of bin b in a table of `buckets` buckets. HASH24: b * C from a
+// full-rate 24-bit multiply, then ((h >> s) * buckets) >> (32 - s) with
+// 2^s >= buckets, so the product stays below 2^32 and the bucket below
+// `buckets`. Else the 32-bit multiplicative hash's high word.
+template <uint32_t kBuckets, bool HASH24>
+GHOSTM_SEED_HD inline uint32_t BinBucket(uint32_t b) {
+  if constexpr (HASH24) {
+    constexpr uint32_t kS = CeilLog2(kBuckets);
+    static_assert(kS >= 8 && kS < 24, "(h >> s) and the bucket count fit 24 bits");
+    const uint32_t h = Mul24(b, 0x9E3779u);
+    return Mul24(h >> kS, kBuckets) >> (32 - kS);
+  } else {
+    return (uint32_t)(((uint64_t)(b * 2654435761u) * kBuckets) >> 32);
   }
 }
 

@@ -81,6 +81,8 @@ class GhostmStats(ctypes.Structure):
         ("traceback_launches_strips", c_uint64),
         ("seconds_traceback_scan", ctypes.c_double),
         ("score_launches_pair", c_uint64),
+        ("seed_table_full", c_uint64),
+        ("seed_compact_redo", c_uint64),
     ]
 
     def as_dict(self) -> dict:
@@ -109,6 +111,8 @@ SIGNATURES = {
     "FreeGpu": (c_int, []),
     "GhostmGetLastError": (c_char_p, []),
     "GhostmBuildInfo": (c_char_p, []),
+    "GhostmDevicePoolTrim": (c_uint64, []),
+    "GhostmDevicePoolInfo": (c_int, [POINTER(c_uint64), POINTER(c_uint64)]),
     "CountCandidatesGpu": (c_int, [c_uint32] * 6 + [u32p]),
     "TraceBackGpu": (c_int, [c_uint32, u32p, u32p, c_uint32, c_uint32, c_int, c_int, u32p, u32p, u32p, POINTER(c_float)]),
     "GhostmBuildIndexGpu": (c_int, [POINTER(ctypes.c_uint8), c_uint32, c_uint32, c_uint32, u32p, u32p, u32p, c_int,
@@ -174,6 +178,13 @@ def load() -> ctypes.CDLL:
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+def device_pool_info() -> tuple[int, int]:
+    """(cached bytes, allocations retried after emptying the cache)."""
+    cached, retries = c_uint64(0), c_uint64(0)
+    load().GhostmDevicePoolInfo(ctypes.byref(cached), ctypes.byref(retries))
+    return cached.value, retries.value
 
 
 def last_error() -> str:

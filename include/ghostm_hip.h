@@ -89,6 +89,16 @@ const char *GhostmGetLastError(void);
 /* Build identity (kernel variant names, arch), for logs. */
 const char *GhostmBuildInfo(void);
 
+/* Device blocks a destroyed session released stay cached for the next session
+ * (at most GHOSTM_DEV_POOL_MB, default 8192 MB). An allocation that runs out of
+ * memory empties the cache and retries once. GhostmDevicePoolTrim frees every
+ * cached block now (for a caller that shares the device with other allocators)
+ * and returns the bytes freed; GhostmDevicePoolInfo reports the cached bytes and
+ * how many allocations were retried after emptying the cache. No reference
+ * counterpart (the reference allocates per Aligner, aligner_gpu.cu). */
+uint64_t GhostmDevicePoolTrim(void);
+int GhostmDevicePoolInfo(uint64_t *cached_bytes, uint64_t *oom_retries);
+
 /* Candidate count of EVERY query of the resident chunk (no batching), K1 count
  * pass; counts[number_query_sequences]. Lets a host reproduce the CPU path's
  * batch cuts exactly (reference aligner.cpp:511-514). */
@@ -207,6 +217,9 @@ typedef struct GhostmStats {
   double seconds_traceback_scan;    /* of seconds_traceback: the scan phase (k_tb_prep, k_tb_pairs, the sorts,
                                        k_tb_scan); the rest is the key DP (k_traceback_key) */
   uint64_t score_launches_pair;     /* K2 launches of sparse segments run by the pair-table kernel (k_score_pair) */
+  uint64_t seed_table_full;         /* K1 queries whose LDS bin table reached its probe bound (redone by the
+                                       table-free merge kernel) */
+  uint64_t seed_compact_redo;       /* K1 compactions re-run by the host (queue overflow, candidate buffers grown) */
 } GhostmStats;
 
 /* Session: parse `aln` options exactly like the reference (getopt string

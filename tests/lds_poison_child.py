@@ -9,8 +9,9 @@ own code) and checks the golden variants under the kernel forms that read LDS:
            K2 forced as paired and as consecutive tasks, and with the sparse
            segments' pair-table K2 forced;
   kernels: every K3 scan mode, every K4 mode, every K1 size class and the
-           offset pass (class caps at the dataset's quartiles, slot cap 2), and
-           the many-segment device pipeline.
+           offset pass (class caps at the dataset's quartiles, slot cap 2), the
+           bin table's probe bound lowered to 0 and 1 windows (the table-free
+           redo), and the many-segment device pipeline.
 
 Prints one JSON line {"runs": n, "failures": [...]} and exits 1 on a mismatch."""
 import hashlib
@@ -83,6 +84,9 @@ def plan(group):
             yield ds, var, opts, env, f"k1_classes_{k1}"
     for ds, var, opts in [("syn_repeat", "default", []), ("syn_scale", "default", [])]:
         yield ds, var, opts, {}, "k1_class3_and_scale"
+    for windows in ("0", "1"):  # the bin table's probe bound and the table-free redo
+        for ds, var, opts in [("syn_small", "default", []), ("syn_dna", "default", [])]:
+            yield ds, var, opts, {"GHOSTM_K1_PROBE_WINDOWS": windows}, f"k1_probe_windows_{windows}"
     for ds, var, opts in [("syn_small", "default", []), ("syn_dna", "default", [])]:
         yield ds, var, opts, {"GHOSTM_SEGMENT_CANDS": "300", "GHOSTM_TAIL_CANDS": "40"}, "segments"
 

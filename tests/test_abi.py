@@ -85,3 +85,12 @@ def test_unsupported_score_option_exits_zero(tmp_path, built):
     assert r.returncode == 0
     assert b"not support score option" in r.stderr
     assert not (tmp_path / "o").exists()
+
+
+def test_library_source_hash_matches_tree(built):
+    """The built libraries report the source hash of this tree (GhostmBuildInfo
+    "src <hash>", ghostm_amd/srchash.py), and ghostm_amd/lib holds only the two
+    product libraries: the GPU suite refuses to run otherwise (conftest.py)."""
+    from conftest import library_hash_mismatch
+
+    assert library_hash_mismatch() is None

@@ -95,6 +95,68 @@ def test_k1_overflow_redo_and_device_offsets(devoff, ds, var, opts, dataset, gol
     assert dev.tobytes() == hits.tobytes()
 
 
+@pytest.mark.parametrize("windows", ["0", "1"])
+@pytest.mark.parametrize("k1", ["filter", "hash"])
+@pytest.mark.parametrize("ds,var,opts", [("syn_small", "default", []), ("syn_dna", "default", []),
+                                         ("syn_scale", "default", []),
+                                         ("syn_small", "b20_t1", ["-b", "20", "-t", "1", "-y", "2"])])
+def test_k1_table_probe_bound_redo(windows, k1, ds, var, opts, dataset, golden):
+    """K1's LDS bin table gives up after a bounded probe (BinTable: every bucket
+    once at most) instead of looping; a query whose insert finds no room is
+    marked kOverflow and redone by a table-free kernel. GHOSTM_K1_PROBE_WINDOWS
+    lowers the bound: 0 fails every insert (every LDS-class query goes filter ->
+    k_seed_hash -> k_seed merge, or k_seed_hash -> k_seed without the filter:
+    GHOSTM_K1=hash, and -t 1: no filter below threshold 2), 1 fails only the bins whose first window is full.
+    Same bytes as the reference either way (the round-5 hang: a bucket outside
+    the table made the old unbounded probe spin forever)."""
+    d = dataset(ds)
+    env = {"GHOSTM_K1_PROBE_WINDOWS": windows}
+    if k1 == "hash":
+        env["GHOSTM_K1"] = "hash"
+    text, st, hits, dev = _run(d, opts, env)
+    assert _sha(text) == golden["aln"][f"{ds}/{var}"]["sha256"]
+    assert dev.tobytes() == hits.tobytes()
+    if windows == "0":
+        assert st["seed_table_full"] > 0, st
+        if k1 == "filter" and var != "b20_t1":  # the filter runs for thresholds >= 2
+            assert st["seed_filter_overflows"] > 0, st
+
+
+@pytest.mark.parametrize("ds,var,opts", [("syn_small", "default", []), ("syn_scale", "default", []),
+                                         ("syn_chunks", "default", [])])
+def test_k1_compaction_with_short_candidate_buffers(ds, var, opts, dataset, golden):
+    """The device compaction behind K1's count read-back runs before the host
+    knows the total: with room for fewer candidates than the run has
+    (GHOSTM_K1_CAND_CAP), it writes only the queries that fit, and the host
+    re-runs the copy into the grown buffers. Same bytes as the reference."""
+    d = dataset(ds)
+    text, st, hits, dev = _run(d, opts, {"GHOSTM_K1_CAND_CAP": "64"})
+    assert _sha(text) == golden["aln"][f"{ds}/{var}"]["sha256"]
+    assert st["seed_compact_redo"] > 0, st
+    assert dev.tobytes() == hits.tobytes()
+
+
+def test_device_pool_out_of_memory_retry(dataset, golden):
+    """Blocks of destroyed sessions stay cached (DevPool); an allocation that
+    runs out of memory empties the cache and retries (GHOSTM_DEV_OOM_TEST fails
+    the first attempt whenever blocks are cached), and GhostmDevicePoolTrim
+    frees the cache on request."""
+    from ghostm_amd import native
+
+    small, scale = dataset("syn_small"), dataset("syn_scale")
+    native.load().GhostmDevicePoolTrim()
+    text, _, _, _ = _run(small, [], {})
+    assert _sha(text) == golden["aln"]["syn_small/default"]["sha256"]
+    cached, retries0 = native.device_pool_info()
+    assert cached > 0
+    text, _, _, _ = _run(scale, [], {"GHOSTM_DEV_OOM_TEST": "1"})
+    assert _sha(text) == golden["aln"]["syn_scale/default"]["sha256"]
+    _, retries1 = native.device_pool_info()
+    assert retries1 > retries0
+    assert native.load().GhostmDevicePoolTrim() > 0
+    assert native.device_pool_info()[0] == 0
+
+
 def test_syn_scale_runs_the_cfg4_classes(dataset, golden):
     """The cfg4 generator's DB with its first 5000 queries, default options: K1
     classes 1 and 2 (k_seed_hash<512,12288>, <1024,24576>) and the offset pass

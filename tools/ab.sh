@@ -1,6 +1,6 @@
 #!/bin/bash
 # Same-box A/B timing: bench.py with the current library (A) and with each
-# alternate build ghostm_amd/lib/libghostm_hip_<tag>.so given as arguments
+# alternate build ab_libs/libghostm_hip_<tag>.so (tools/altlib.sh) given as arguments
 # (default: prev), alternating, N rounds (AB_ROUNDS, default 2). AB_ARGS adds
 # bench options (e.g. "--queries 125000"). The data set is generated once.
 set -euo pipefail
@@ -12,7 +12,7 @@ mkdir -p "$R/gpurun_out/ab" /tmp/ghostm_ab_data
 for i in $(seq 1 "$N"); do
   timeout -k 10 200 python3 "$R/bench.py" $ARGS > "$R/gpurun_out/ab/A$i.log" 2>&1
   for t in $TAGS; do
-    GHOSTM_LIB_PATH="$R/ghostm_amd/lib/libghostm_hip_$t.so" \
+    GHOSTM_LIB_PATH="$R/ab_libs/libghostm_hip_$t.so" \
       timeout -k 10 200 python3 "$R/bench.py" $ARGS > "$R/gpurun_out/ab/${t}$i.log" 2>&1
   done
 done
