@@ -1650,6 +1650,11 @@ size_t Session::DeviceHits(void *dst, size_t cap) {
 void Session::PartDone(const Part *part) {
   if (stream_fd_ < 0) return;
   writer_->Submit([this, part] {
+    TraceMark("w_begin", stream_off_);
+    struct Done {
+      const uint64_t &off;
+      ~Done() { TraceMark("w_end", off); }
+    } done{stream_off_};
     for (const std::string &t : part->text) {
       const char *p = t.data();
       size_t left = t.size();

@@ -48,6 +48,22 @@ def counters(d: str) -> dict:
     return vals, dur
 
 
+def library_hash() -> dict:
+    """The profiled library's GhostmBuildInfo and source hash (ghostm_amd/srchash.py):
+    bench.py uses these counters only while it times a library with the same hash."""
+    import ctypes
+    import sys
+
+    sys.path.insert(0, REPO)
+    from ghostm_amd import native, srchash
+
+    lib = ctypes.CDLL(native.LIB_PATH)
+    lib.GhostmBuildInfo.restype = ctypes.c_char_p
+    info = lib.GhostmBuildInfo().decode()
+    return {"library": os.path.relpath(native.LIB_PATH, REPO), "library_build_info": info,
+            "library_src_hash": srchash.info_hash(info), "tree_src_hash": srchash.tree_hash()}
+
+
 def mean(xs):
     xs = list(xs)
     return sum(xs) / len(xs) if xs else None
@@ -116,9 +132,10 @@ def main() -> None:
             if c.get("SQ_LDS_IDX_ACTIVE") and c.get("SQ_LDS_BANK_CONFLICT") is not None:
                 busy = c["SQ_LDS_IDX_ACTIVE"] - c["SQ_LDS_BANK_CONFLICT"]
                 e["lds_bank_conflict_rate"] = c["SQ_LDS_BANK_CONFLICT"] / busy if busy > 0 else None
+    lib = library_hash()
     with open(os.path.join(prof, f"{args.round}_pmc.json"), "w") as f:
-        json.dump({"round": args.round, "queries": args.queries, "preset": args.preset, "kernels": kernels}, f,
-                  indent=1, sort_keys=True)
+        json.dump({"round": args.round, "queries": args.queries, "preset": args.preset, **lib, "kernels": kernels},
+                  f, indent=1, sort_keys=True)
 
     def fam(prefix):
         best = [k for k in kernels if k.startswith(prefix) and "hbm_bytes_per_launch" in kernels[k]]
@@ -135,7 +152,7 @@ def main() -> None:
     k1v_step = sum(kernels[k]["valu_insts_per_launch"] * kernels[k].get("launches_in_trace", 0) for k in k1v)
     k2 = [k for k in kernels if k.startswith("k_score") and "valu_insts_per_launch" in kernels[k]]
     k2_main = max(k2, key=lambda x: kernels[x].get("percent_of_gpu_time", 0)) if k2 else None
-    traffic = {"round": args.round, "queries": args.queries, "preset": args.preset,
+    traffic = {"round": args.round, "queries": args.queries, "preset": args.preset, **lib,
                "note": "HBM bytes per launch = FETCH_SIZE*2*1024 + WRITE_SIZE*1024 (gfx950 correction); "
                        "VALU instructions = SQ_INSTS_VALU per dispatch",
                "k_score_hbm_bytes_per_launch": fam("k_score"),
