@@ -565,6 +565,7 @@ void Session::Create(uint32_t shard_rank, uint32_t shard_world, const ShardExcha
     AgreeOnCreate(shard_rank, shard_world, *ex, err, chunk_nseq, rank_lo);
     PlanExchange(shard_rank, shard_world, *ex, chunk_nseq, rank_lo);
   }
+  TraceMark("create_sync");
   DeviceModule::Get().Synchronize();
   TraceMark("uploaded");
   formatter_.reset(new TaskQueue());
@@ -750,6 +751,7 @@ void Session::Load(uint32_t shard_rank, uint32_t shard_world, bool local, std::v
     for (size_t k = 0; k < dbs_.size(); ++k)
       if (dbs_[k].chunk.id != k) throw Error("DB chunk ids out of order");
     dev.SetChunkBases(bases.data(), (uint32_t)bases.size());
+    TraceMark("bases_set");
   }
 
   if (local) {
@@ -816,6 +818,7 @@ void Session::Load(uint32_t shard_rank, uint32_t shard_world, bool local, std::v
     if (!q.dev) upload_query(q);  // (uploaded while reading when unsharded)
     q.chunk.seq.Release();  // resident on the device (qlen and names stay on the host)
   }
+  TraceMark("queries_released");
   // query chunks read past a missing one are not used (freed by `unadopted`)
 }
 

@@ -204,6 +204,19 @@ __device__ inline uint32_t BlockExclusiveScan(uint32_t v, uint32_t *s_part, uint
   return r;
 }
 
+// Exclusive prefix of v over the 64 lanes of one wave; *total = the wave's sum.
+__device__ inline uint32_t WaveExclusiveScan(uint32_t v, uint32_t *total) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  *total = __builtin_amdgcn_readlane(x, 63);
+  return x - v;
+}
+
 // Length of the run of `key` starting at i in sorted S[0..n).
 __device__ inline uint32_t RunLength(const uint32_t *S, uint32_t n, uint32_t i, uint32_t key) {
   uint32_t k = i;
@@ -715,6 +728,15 @@ __host__ __device__ constexpr uint32_t FilterWords(uint32_t fslots) { return fsl
 #ifndef GHOSTM_K1_MBCNT
 #define GHOSTM_K1_MBCNT 1
 #endif
+// Phase 0 and the emission without block scans (GHOSTM_K1_WAVESCAN=0 keeps
+// them, A/B): with at most 64 lists (L = 127: 62) the list offsets are one
+// wave's scan, published by the phase's one barrier; the emission takes each
+// wave's run of s_emit positions with one LDS atomic (the bins are ranked by
+// value afterwards, so their order there is free). One barrier each instead of
+// three and thread 0's serial pass over the waves' partial sums.
+#ifndef GHOSTM_K1_WAVESCAN
+#define GHOSTM_K1_WAVESCAN 1
+#endif
 // Pass 2 (A/B): the filter test without branches
 #ifndef GHOSTM_K1_P2BF
 #define GHOSTM_K1_P2BF 0
@@ -796,7 +818,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   __shared__ uint8_t s_cfirst[kChunks];
   __shared__ __attribute__((aligned(16))) uint32_t s_emit[kMaxSlotCap];
   __shared__ uint32_t s_part[kW];
-  __shared__ uint32_t s_total, s_qn, s_full;
+  __shared__ uint32_t s_total, s_qn, s_full, s_nemit;
 
   const uint32_t q = SeedBlockQuery(a);
   if (q == kNoQuery) return;
@@ -810,13 +832,23 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   if (tid == 0) {
     s_qn = 0;
     s_full = 0;
+    s_nemit = 0;
   }
   uint32_t len = 0, beg = 0;
   if (tid < nl) {
     beg = a.list_beg[(size_t)q * nl + tid];
     len = a.list_len[(size_t)q * nl + tid];
   }
-  const uint32_t excl = BlockExclusiveScan(len, s_part, &s_total);
+  uint32_t excl = 0;
+  if (GHOSTM_K1_WAVESCAN && nl <= 64) {  // block-uniform: every list in wave 0
+    if (wave == 0) {
+      uint32_t total;
+      excl = WaveExclusiveScan(len, &total);
+      if (tid == 0) s_total = total;  // (read by thread 0 itself below)
+    }
+  } else {
+    excl = BlockExclusiveScan(len, s_part, &s_total);
+  }
   if (tid < nl) {
     s_off[tid] = excl;
     if constexpr (kPrevAll) {
@@ -1247,8 +1279,19 @@ __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
       ++mine;
     }
   }
-  const uint32_t base = BlockExclusiveScan(mine, s_part, &s_total);
-  const uint32_t total = s_total;
+  uint32_t base, total;
+  if constexpr (GHOSTM_K1_WAVESCAN) {
+    uint32_t wsum;
+    base = WaveExclusiveScan(mine, &wsum);
+    uint32_t wbase = 0;
+    if (lane == 0 && wsum) wbase = atomicAdd(&s_nemit, wsum);
+    base += __builtin_amdgcn_readfirstlane(wbase);
+    __syncthreads();
+    total = s_nemit;
+  } else {
+    base = BlockExclusiveScan(mine, s_part, &s_total);
+    total = s_total;
+  }
   if (tid == 0) a.counts[q] = total;
   if (total == 0 || total > a.slot_cap) return;  // offset pass redoes the wide ones
   uint32_t at = base;

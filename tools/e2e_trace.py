@@ -20,6 +20,20 @@ from ghostm_amd import workloads  # noqa: E402
 from ghostm_amd.aligner import Session  # noqa: E402
 
 
+def cpu_stat() -> dict:
+    """The cgroup's CPU counters (cgroup v2 cpu.stat): throttling shows as
+    nr_throttled / throttled_usec growing across a run."""
+    out = {}
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            for line in f:
+                k, v = line.split()
+                out[k] = int(v)
+    except OSError:
+        pass
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--preset", default="cfg2")
@@ -40,13 +54,16 @@ def main() -> None:
         os.sync()
         time.sleep(args.settle)
         print(f"=== run {k}", file=sys.stderr, flush=True)
+        c0 = cpu_stat()
         t0 = time.perf_counter()
         with Session(argv) as s:
             t1 = time.perf_counter()
             s.run(to_file=True)
             t2 = time.perf_counter()
+        c1 = cpu_stat()
+        d = {k: c1[k] - c0.get(k, 0) for k in ("nr_throttled", "throttled_usec", "usage_usec") if k in c1}
         print(f"e2e run {k}: create {1e3 * (t1 - t0):.2f} ms, run+write {1e3 * (t2 - t1):.2f} ms, "
-              f"total {1e3 * (t2 - t0):.2f} ms, file {os.path.getsize(out)} bytes", flush=True)
+              f"total {1e3 * (t2 - t0):.2f} ms, file {os.path.getsize(out)} bytes, cpu {d}", flush=True)
 
 
 if __name__ == "__main__":
