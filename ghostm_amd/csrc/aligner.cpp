@@ -109,6 +109,25 @@ void ParallelFor(size_t n, unsigned threads,
   WorkerPool::Get().Run(pieces, [&](unsigned t) { fn(t * per, std::min(n, (size_t)t * per + per), t); });
 }
 
+size_t PieceCount(size_t n, size_t pieces) {
+  if (n == 0) return 0;
+  const size_t per = (n + std::max<size_t>(1, std::min(pieces, n)) - 1) / std::max<size_t>(1, std::min(pieces, n));
+  return (n + per - 1) / per;
+}
+
+void ParallelForPieces(size_t n, size_t pieces, unsigned threads,
+                       const std::function<void(size_t, size_t, unsigned)> &fn) {
+  const size_t np = PieceCount(n, pieces);
+  if (np == 0) return;
+  const size_t per = (n + np - 1) / np;
+  if (threads <= 1 || np == 1) {
+    for (size_t t = 0; t < np; ++t) fn(t * per, std::min(n, t * per + per), (unsigned)t);
+    return;
+  }
+  WorkerPool::Get().Run((unsigned)np, [&](unsigned t) { fn(t * per, std::min(n, (size_t)t * per + per), t); },
+                        threads);
+}
+
 // ------------------------------------------------------------------ TaskQueue
 TaskQueue::TaskQueue() : worker_([this] { Loop(); }) {}
 
@@ -1408,6 +1427,16 @@ struct TextCursor {
 };
 }  // namespace
 
+// pieces per formatting worker in a streamed run (GHOSTM_STREAM_PIECES, A/B;
+// 1 = the part's pieces as in a run without a file)
+static size_t StreamPiecesPerWorker() {
+  static const size_t v = [] {
+    const char *e = getenv("GHOSTM_STREAM_PIECES");
+    return e ? (size_t)std::max(1, atoi(e)) : (size_t)4;
+  }();
+  return v;
+}
+
 const LineFormat &Session::Format() {
   if (!format_) format_.reset(new LineFormat(opt_.output_style, opt_.karlin, 4095));
   return *format_;
@@ -1418,6 +1447,32 @@ void Session::Part::Reset(size_t pieces) {
   hits.resize(pieces);
   for (std::string &t : text) t.clear();
   for (std::vector<GhostmHit> &h : hits) h.clear();
+  std::lock_guard<std::mutex> lk(mu);
+  done.assign(pieces, 0);
+  abandoned = false;
+  streaming = false;
+}
+
+void Session::Part::MarkDone(size_t k) {
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    done[k] = 1;
+  }
+  cv.notify_all();
+}
+
+void Session::Part::Abandon() {
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    abandoned = true;
+  }
+  cv.notify_all();
+}
+
+bool Session::Part::Wait(size_t k) {
+  std::unique_lock<std::mutex> lk(mu);
+  cv.wait(lk, [&] { return done[k] || abandoned; });
+  return done[k] != 0;
 }
 
 Session::Part *Session::NewPart() {
@@ -1454,13 +1509,26 @@ void Session::FormatSelected(const QueryData &q, uint32_t g0, const std::vector<
                              const HostHits &hits, uint32_t cap, Part *out) {
   const uint32_t ng = (uint32_t)counts.size();
   const unsigned workers = std::max(1u, threads_ > 1 ? threads_ - 1 : 1u);
-  out->Reset(workers);
+  // a streamed run cuts the part into four pieces per worker, formatted in
+  // order, and the writer writes each as soon as it and those before it are
+  // done (the file then trails the formatting by a piece, not by the part)
+  const bool stream = stream_fd_ >= 0;
+  const size_t pieces = PieceCount(ng, stream ? (size_t)workers * StreamPiecesPerWorker() : workers);
+  out->Reset(pieces);
+  struct AbandonOnError {  // a failed formatting releases the writer waiting for its pieces
+    Part *p;
+    bool armed = true;
+    ~AbandonOnError() {
+      if (armed) p->Abandon();
+    }
+  } abandon{out};
+  if (stream) StreamPart(out);
   const LineFormat &w = Format();
   // timeline diagnostics: each worker's wall and on-CPU time (a thread that
   // waits for a CPU, e.g. under a cgroup quota, shows wall >> CPU)
   const bool trace = TraceOn();
   std::vector<double> wall(trace ? workers : 0), cpu(trace ? workers : 0);
-  ParallelFor(ng, workers, [&](size_t b, size_t e, unsigned t) {
+  ParallelForPieces(ng, pieces, workers, [&](size_t b, size_t e, unsigned t) {
     const double w0 = trace ? NowSeconds() : 0.0, c0 = trace ? ThreadCpuSeconds() : 0.0;
     struct Done {
       bool on;
@@ -1474,6 +1542,7 @@ void Session::FormatSelected(const QueryData &q, uint32_t g0, const std::vector<
     for (size_t g = b; g < e; ++g) nh += counts[g];
     out->text[t].reserve(nh * 96);
     ph.reserve(nh);
+    {
     TextCursor text(out->text[t]);
     for (size_t g = b; g < e; ++g) {
       const uint32_t i = q.group_last[g0 + g];
@@ -1492,7 +1561,10 @@ void Session::FormatSelected(const QueryData &q, uint32_t g0, const std::vector<
                                seq_id});
       }
     }
+    }  // the piece's text is final here (TextCursor trims it)
+    if (stream) out->MarkDone(t);
   });
+  abandon.armed = false;
   if (trace) {
     double ws = 0, cs = 0, wm = 0;
     for (unsigned t = 0; t < workers; ++t) ws += wall[t], cs += cpu[t], wm = std::max(wm, wall[t]);
@@ -1650,8 +1722,37 @@ size_t Session::DeviceHits(void *dst, size_t cap) {
   return n;
 }
 
+// The writer's task for a streamed part: piece k is written once it is
+// formatted (Part::Wait), in order; submitted before the formatting starts, so
+// the writer's tasks stay in part order.
+void Session::StreamPart(Part *part) {
+  part->streaming = true;
+  writer_->Submit([this, part] {
+    TraceMark("w_begin", stream_off_);
+    struct Done {
+      const uint64_t &off;
+      ~Done() { TraceMark("w_end", off); }
+    } done{stream_off_};
+    for (size_t k = 0; k < part->text.size(); ++k) {
+      if (!part->Wait(k)) return;  // formatting failed: the run throws from the formatter
+      const char *p = part->text[k].data();
+      size_t left = part->text[k].size();
+      while (left && !stream_failed_) {
+        const ssize_t w = pwrite(stream_fd_, p, left, (off_t)stream_off_);
+        if (w <= 0) {
+          stream_failed_ = true;
+          break;
+        }
+        p += w;
+        left -= (size_t)w;
+        stream_off_ += (uint64_t)w;
+      }
+    }
+  });
+}
+
 void Session::PartDone(const Part *part) {
-  if (stream_fd_ < 0) return;
+  if (stream_fd_ < 0 || part->streaming) return;  // (a streamed part is written by StreamPart's task)
   writer_->Submit([this, part] {
     TraceMark("w_begin", stream_off_);
     struct Done {

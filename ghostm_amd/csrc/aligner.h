@@ -91,6 +91,11 @@ struct ShardExchange {
 
 // Parallel for over [0, n) in contiguous blocks.
 void ParallelFor(size_t n, unsigned threads, const std::function<void(size_t, size_t, unsigned)> &fn);
+// ... in PieceCount(n, pieces) contiguous blocks, claimed in order by at most
+// `threads` threads (fn's third argument is the block's index)
+size_t PieceCount(size_t n, size_t pieces);
+void ParallelForPieces(size_t n, size_t pieces, unsigned threads,
+                       const std::function<void(size_t, size_t, unsigned)> &fn);
 
 // One background thread running submitted tasks in order.
 class TaskQueue {
@@ -172,7 +177,17 @@ class Session {
   struct Part {
     std::vector<std::string> text;
     std::vector<std::vector<GhostmHit>> hits;
+    // a streamed run (FormatSelected) writes each piece as soon as it is
+    // formatted, in order: the formatting workers mark pieces done, the writer
+    // waits for the next one; Abandon (formatting failed) releases the writer
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<uint8_t> done;
+    bool abandoned = false, streaming = false;
     void Reset(size_t pieces);
+    void MarkDone(size_t k);
+    void Abandon();
+    bool Wait(size_t k);  // false: abandoned before piece k was formatted
   };
   using Results = std::vector<std::vector<HitRecord>>;
 
@@ -207,6 +222,7 @@ class Session {
   Part *NewPart();
   // a part's text is complete: hands it to the output writer when streaming
   void PartDone(const Part *part);
+  void StreamPart(Part *part);
   const LineFormat &Format();
 
   AlignerOptions opt_;

@@ -323,7 +323,8 @@ constexpr uint32_t kFilterScale = kFilterAlias ? 2 : 1;
 #define GHOSTM_FILTER2 kern::k_seed_filter<1024, 131072 * kFilterScale, 9216, 6144, kFilterAlias, kFilterStage2>
 constexpr size_t FilterLds(size_t cells, size_t table, size_t queue) {
   const size_t words = kern::FilterWords((uint32_t)cells);
-  return ((kFilterAlias ? std::max(words, table) : words + table) + queue) * 4;
+  const size_t region = (kFilterAlias ? std::max(words, table) : words + table) + queue;
+  return kern::FilterStaticLds((uint32_t)region) ? 0 : region * 4;  // dynamic LDS bytes
 }
 constexpr size_t kFilterLds0 = FilterLds(32768 * kFilterScale, 2304, 1536);
 constexpr size_t kFilterLds1 = FilterLds(65536 * kFilterScale, 4608, 3072);

@@ -792,13 +792,24 @@ __host__ __device__ constexpr uint32_t Log2(uint32_t v) {
   while ((1u << (l + 1)) <= v) ++l;
   return l;
 }
+// k_seed_filter's region as static LDS (GHOSTM_K1_STATIC=0: always dynamic, A/B)
+#ifndef GHOSTM_K1_STATIC
+#define GHOSTM_K1_STATIC 1
+#endif
+__host__ __device__ constexpr bool FilterStaticLds(uint32_t words) { return GHOSTM_K1_STATIC && words * 4 <= 56 * 1024; }
 template <uint32_t BLOCK, uint32_t FSLOTS, uint32_t TSLOTS, uint32_t QCAP, bool ALIAS = false, bool STAGE2 = false>
 __global__ __launch_bounds__(BLOCK) void k_seed_filter(SeedArgs a) {
   GHOSTM_POISON_LDS();
-  extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
   constexpr uint32_t kFWords = FSLOTS / 16;   // 16 two-bit cells per word
   constexpr uint32_t kFWordsPad = FilterWords(FSLOTS);  // + the READ2 guard word
   constexpr uint32_t kRegion = ALIAS ? (kFWordsPad > TSLOTS ? kFWordsPad : TSLOTS) : kFWordsPad + TSLOTS;
+  // the bitmap/table/queue region: a static array when it fits (its address is
+  // a constant the LDS instructions take as their offset, no base add per
+  // access; FilterStaticLds), else the dynamic allocation
+  constexpr bool kStaticRegion = FilterStaticLds(kRegion + QCAP);
+  __shared__ __attribute__((aligned(16))) uint32_t s_static[kStaticRegion ? kRegion + QCAP : 4];
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_extern[];
+  uint32_t *const s_dyn = kStaticRegion ? s_static : s_extern;
   constexpr uint32_t kF2Words = STAGE2 ? FloorPow2(kRegion - TSLOTS) : 0;  // second bitmap (words)
   static_assert(!STAGE2 || (ALIAS && kF2Words >= 64), "the second bitmap lives past the aliased table");
   constexpr uint32_t kF2Bits = STAGE2 ? Log2(kF2Words * 16) : 1;

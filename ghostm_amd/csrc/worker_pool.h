@@ -25,13 +25,15 @@ class WorkerPool {
     return *pool;
   }
 
-  void Run(unsigned pieces, const std::function<void(unsigned)> &fn) {
+  // pieces 0 .. pieces-1 of fn, claimed in order; the pool grows to at most
+  // max_threads - 1 workers for it (the caller works too)
+  void Run(unsigned pieces, const std::function<void(unsigned)> &fn, unsigned max_threads = ~0u) {
     Job job;
     job.fn = &fn;
     job.n = pieces;
     job.errors.resize(pieces);
     std::unique_lock<std::mutex> lk(mu_);
-    Grow(pieces - 1);
+    Grow(std::min(pieces, std::max(max_threads, 1u)) - 1);
     jobs_.push_back(&job);
     lk.unlock();
     cv_.notify_all();
