@@ -1670,6 +1670,7 @@ void Session::Run(bool stream_to_file) {
   stats_.seed_filter_overflows = dt.seed_filter_overflows;
   stats_.seed_table_full = dt.seed_table_full;
   stats_.seed_compact_redo = dt.seed_compact_redo;
+  stats_.score_launches_sparse = dt.score_launches_sparse;
   stats_.score_launches_swar = dt.score_launches_swar;
   stats_.score_launches_unit = dt.score_launches_unit;
   stats_.score_launches_pair = dt.score_launches_pair;

@@ -215,6 +215,7 @@ struct DevDb {
   DevBuf seq, kc, pos;
   DevBuf low;                      // kern::k_low_keys' bitmap
   uint32_t len = 0, kcl = 0, npos = 0;
+  bool codes_le26 = false;         // every residue code <= 26 (the sparse K2 profiles hold rows 0..26)
   const uint8_t *Residues() const { return seq.as<uint8_t>() + kDbFront; }
   DevBuf subj;                     // subject starts (device merge)
   DevBuf subj_bucket;              // kern::SubjectOfBucketed's table
@@ -263,6 +264,7 @@ struct DeviceModule::Impl {
     bool swar = false, pairs_ok = true;
     uint32_t per_block = 0;
     size_t bytes = 0;
+    uint32_t sparse_per_block = 0;
   } deferred;
   // K3 work (tb_sort: two histograms + total, two cursor arrays)
   DevBuf tb_qid, tb_end, tb_start, tb_ml;
@@ -410,6 +412,10 @@ void DeviceModule::Bind(int device) {
                                 (int)kFilterLds1));
   HIP_CHECK(hipFuncSetAttribute((const void *)GHOSTM_FILTER2, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)kFilterLds2));
+  // the sparse rows K2 (kScoreRowsSparse): seven 27-row profiles, ~53 KB at L = 127
+  HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_score16f<16, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)(kern::kScoreQmaxSparse * kern::kProfRowsSparse * ((kMaxQueryLength + 15) / 16 * 16 + 8) * 2 +
+                                      32 * 32 * 2)));
   const int scan_lds = (int)kScanLds;
 #define GHOSTM_SCAN_ATTR(SS, HH, EE, FF)                                             \
   HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_tb_scan<SS, HH, EE, FF>,       \
@@ -548,6 +554,7 @@ DevDb *DeviceModule::UploadDb(const uint8_t *seq, uint32_t len, const uint32_t *
   Use();
   if (!impl_) throw Error("device not bound");
   // the kernels index 32-entry tables by residue code (checked 8 bytes at a time)
+  uint64_t over26 = 0;  // a byte >= 27 sets its top bit in (byte + 101) (codes < 32 do not carry)
   {
     uint64_t hi = 0;
     uint32_t k = 0;
@@ -555,11 +562,16 @@ DevDb *DeviceModule::UploadDb(const uint8_t *seq, uint32_t len, const uint32_t *
       uint64_t w;
       std::memcpy(&w, seq + k, 8);
       hi |= w;
+      over26 |= (w & 0x1F1F1F1F1F1F1F1Full) + 0x6565656565656565ull;
     }
-    for (; k < len; ++k) hi |= seq[k];
+    for (; k < len; ++k) {
+      hi |= seq[k];
+      over26 |= (uint64_t)((seq[k] & 0x1Fu) + 0x65u);
+    }
     if (hi & 0xE0E0E0E0E0E0E0E0ull) throw Error("database residue code out of range");
   }
   DevDb *d = new DevDb();
+  d->codes_le26 = (over26 & 0x8080808080808080ull) == 0;
   d->len = len;
   d->kcl = kcl;
   d->npos = npos;
@@ -1110,6 +1122,19 @@ uint32_t DeviceModule::ScorePerBlock(DevQuery *q, uint32_t base, const GapConfig
   return (kern::kScoreBlock / 64) * lay.gpw * (ScorePacked(impl_->h_matrix, q->L, base, gap) ? 2 : 1);
 }
 
+// The sparse rows kernel's layout (16 rows per lane) and its candidates per
+// block; per_block 0 when it cannot run (a DB code above 26, or more than 16
+// lanes per candidate)
+static Layout SparseLayout(uint32_t L) {
+  const uint32_t G = (L + 15) / 16;
+  return Layout{16, G, G * 16, G ? 64 / G : 64};
+}
+static uint32_t SparsePerBlock(const DevQuery *q, const DevDb *d) {
+  const Layout s = SparseLayout(q->L);
+  if (!d->codes_le26 || s.G == 0 || s.G > 16) return 0;
+  return (kern::kScoreBlock / 64) * s.gpw * 2;
+}
+
 // K2 in two steps for the device-merge pipeline: ScoreLaunch enqueues the
 // launch (no host wait) and prepares the next segment's tasks; ScoreFinish
 // waits for it, reads its counters on the copy stream (the main stream may
@@ -1153,6 +1178,7 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
   int guard = swar ? 0 : framed ? (bound + sigma_max < 2040 ? 0 : (int)(2040 - sigma_max)) : (bound < 2048 ? 0 : 2000);
   if (half && getenv("GHOSTM_K2_GUARD")) guard = atoi(getenv("GHOSTM_K2_GUARD"));  // tests: force re-scores
   const uint32_t per_block = ScorePerBlock(q, base, gap);
+  const uint32_t sparse_pb = swar ? SparsePerBlock(q, d) : 0u;
   // tasks, and with them the kernel (score_tasks.h BuildTasks: the unit-pair
   // kernel where its blocks are not too many more): prepared for this range by
   // the previous launch (uploaded on the copy stream into the other task
@@ -1162,7 +1188,8 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
   size_t ntasks = 0;
   // staging and task buffers hold ScoreTaskBound tasks, or n pair entries
   auto task_bytes = [&](uint64_t cn, uint32_t q0, uint32_t q1) {
-    return std::max<size_t>(ScoreTaskBound(cn, q0, q1, per_block, kern::kScoreQmaxUnit) * sizeof(kern::ScoreTask),
+    const uint32_t pb = sparse_pb ? std::min(per_block, sparse_pb) : per_block;
+    return std::max<size_t>(ScoreTaskBound(cn, q0, q1, pb, kern::kScoreQmaxUnit) * sizeof(kern::ScoreTask),
                             (size_t)cn * 4);
   };
   if (I.prepared.valid && I.prepared.cand_begin == cand_begin && I.prepared.n == n &&
@@ -1182,7 +1209,7 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
     PinnedBuf &hs = I.h_tasks[buf];
     hs.Reserve(task_bytes(n, q_first, q_end));
     ntasks = BuildTasks(swar, cand_begin, n, q_first, q_end, counts, offsets, per_block, hs.as<kern::ScoreTask>(),
-                        &kind, guard == 0, &host_par_);
+                        &kind, guard == 0, &host_par_, sparse_pb);
     TraceMark("tasks", ntasks);
     if (const char *dump = getenv("GHOSTM_DEBUG_TASKS")) {  // diagnostics: the launch's tasks and counts
       if (FILE *f = fopen(dump, "ab")) {
@@ -1200,7 +1227,8 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
     TraceMark("tasks_up", ntasks);
   }
   I.task_turn = 1 - buf;
-  const bool unit = kind == kScoreUnit, pairs = kind == kScorePairs;
+  const bool unit = kind == kScoreUnit, pairs = kind == kScorePairs, sparse = kind == kScoreRowsSparse;
+  const Layout slay = SparseLayout(q->L);
   if (pairs && q->fcodes_lpad != lay.Lpad) {  // the query chunk's forward row codes, once
     q->fcodes.Reserve((size_t)q->nseq * lay.Lpad + 16);
     const size_t words = (size_t)q->nseq * (lay.Lpad / 4);
@@ -1238,6 +1266,14 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
     a.npairs = (uint32_t)ntasks;
     a.fcodes = q->fcodes.as<uint32_t>();
   }
+  if (sparse) {  // 16 rows per lane, kScoreQmaxSparse profiles of kProfRowsSparse code rows
+    a.Lpad = slay.Lpad;
+    a.pad = slay.Lpad - q->L;
+    a.G = slay.G;
+    a.gpw = slay.gpw;
+    a.prof_slots = kern::SparseSlots();
+    a.prof_rows = kern::kProfRowsSparse;
+  }
   // counters: [0] cells (u64), [2] guard count (u32)
   I.counters.Reserve(32);
   HIP_CHECK(hipMemsetAsync(I.counters.p, 0, 32, S(stream_)));
@@ -1251,6 +1287,7 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
   // packed: the profiles, then the 32 x 32 code table they are built from
   // (UNIT: 32-bit words, rows padded by 4 words, a 32 x 32 word code table)
   const size_t lds = unit     ? (size_t)kern::kScoreQmaxUnit * kern::kProfRows16 * (lay.Lpad + 4) * 4 + 32 * 32 * 4
+                     : sparse ? (size_t)kern::SparseSlots() * kern::kProfRowsSparse * (slay.Lpad + 8) * 2 + 32 * 32 * 2
                      : packed ? (size_t)kern::kScoreQmax * kern::kProfRows16 * (lay.Lpad + 8) * 2 + 32 * 32 * 2
                               : (size_t)kern::kScoreQmax * kern::kProfRows * (lay.Lpad + 4) * 4;
   HIP_CHECK(hipEventRecord(I.ev0, S(stream_)));
@@ -1277,6 +1314,8 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
       case 16: hipLaunchKernelGGL((kern::k_score_pair<16>), pgrid, pblock, plds, S(stream_), a); break;
       default: hipLaunchKernelGGL((kern::k_score_pair<8>), pgrid, pblock, plds, S(stream_), a); break;
     }
+  } else if (sparse) {
+    hipLaunchKernelGGL((kern::k_score16f<16, true>), grid, block, lds, S(stream_), a);
   } else if (packed) {
     switch (lay.S) {
       case 32:
@@ -1317,6 +1356,7 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
   times_.score_launches_swar += swar ? 1 : 0;
   times_.score_launches_unit += unit ? 1 : 0;
   times_.score_launches_pair += pairs ? 1 : 0;
+  times_.score_launches_sparse += sparse ? 1 : 0;
   P.active = true;
   P.guarded = half && guard;
   P.cand_begin = cand_begin;
@@ -1333,7 +1373,7 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
   I.deferred = Impl::DeferredNext{};
   if (next && next->n) {
     I.deferred = Impl::DeferredNext{true, *next, swar, guard == 0, per_block,
-                                    task_bytes(next->n, next->q_first, next->q_end)};
+                                    task_bytes(next->n, next->q_first, next->q_end), sparse_pb};
     if (!defer_next_) ScorePrepareNext(counts, offsets);
   }
 }
@@ -1349,7 +1389,8 @@ void DeviceModule::ScorePrepareNext(const std::vector<uint32_t> &counts, const s
   int nkind = kScoreRows;
   hs.Reserve(dn.bytes);
   const size_t nt = BuildTasks(dn.swar, next->cand_begin, next->n, next->q_first, next->q_end, counts, offsets,
-                               dn.per_block, hs.as<kern::ScoreTask>(), &nkind, dn.pairs_ok);
+                               dn.per_block, hs.as<kern::ScoreTask>(), &nkind, dn.pairs_ok, nullptr,
+                               dn.sparse_per_block);
   const size_t nbytes = nt * (nkind == kScorePairs ? 4 : sizeof(kern::ScoreTask));
   I.task_buf[nb].Reserve(nbytes);
   HIP_CHECK(hipMemcpyAsync(I.task_buf[nb].p, hs.p, nbytes, hipMemcpyHostToDevice, S(copy_stream_)));

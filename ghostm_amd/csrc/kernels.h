@@ -1459,7 +1459,12 @@ struct ScoreArgs {
   const uint32_t *pairs;
   uint32_t npairs;
   const uint32_t *fcodes;
+  // k_score16f<S, true> over sparse segments (kScoreRowsSparse): the profile
+  // slots per block and code rows per slot (0 = kScoreQmax, kProfRows16)
+  uint32_t prof_slots, prof_rows;
 };
+__device__ inline uint32_t ProfSlots(const ScoreArgs &a) { return a.prof_slots ? a.prof_slots : (uint32_t)kScoreQmax; }
+__device__ inline uint32_t ProfRows(const ScoreArgs &a) { return a.prof_rows ? a.prof_rows : kProfRows16; }
 
 template <int S>
 __global__ __launch_bounds__(kScoreBlock) void k_score(ScoreArgs a) {
@@ -1737,7 +1742,8 @@ __device__ inline uint32_t MulU24(uint32_t a, uint32_t b) {
 template <class C, bool FRAMED, bool SWAR = false>
 __device__ __forceinline__ void BuildProfile16(const ScoreArgs &a, const ScoreTask &t, short *s_prof16,
                                                uint32_t RS) {
-  short *s_enc = s_prof16 + kScoreQmax * kProfRows16 * RS;
+  const uint32_t nrows = ProfRows(a);  // code rows per slot: 32, or 27 (codes 0..26) for the sparse blocks
+  short *s_enc = s_prof16 + ProfSlots(a) * nrows * RS;
   const int extp = -a.ext;
   const uint32_t drop = SWAR ? (uint32_t)(0x10000u - (a.swar_low - 64u)) & 0xFFFFu : 0u;
   for (uint32_t e = threadIdx.x; e < 32 * 32; e += kScoreBlock) {
@@ -1755,7 +1761,7 @@ __device__ __forceinline__ void BuildProfile16(const ScoreArgs &a, const ScoreTa
   const uint32_t rows = t.q_count * a.Lpad;
   for (uint32_t p = threadIdx.x; p < rows; p += kScoreBlock) {
     const uint32_t slot = p / a.Lpad, r = p - slot * a.Lpad;
-    short *dst = s_prof16 + slot * kProfRows16 * RS + r;
+    short *dst = s_prof16 + slot * nrows * RS + r;
     uint32_t w[16];
     if (r < a.pad) {
 #pragma unroll
@@ -1775,7 +1781,8 @@ __device__ __forceinline__ void BuildProfile16(const ScoreArgs &a, const ScoreTa
       }
     }
 #pragma unroll
-    for (int c = 0; c < 32; ++c) dst[c * RS] = (short)((c & 1) ? w[c >> 1] >> 16 : w[c >> 1]);
+    for (int c = 0; c < 32; ++c)
+      if ((uint32_t)c < nrows) dst[c * RS] = (short)((c & 1) ? w[c >> 1] >> 16 : w[c >> 1]);
   }
 }
 
@@ -2099,8 +2106,9 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
   typedef __attribute__((address_space(3))) const u32x4 lds_u4;
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char *)s_prof16;
   constexpr uint32_t EB = UNIT ? 4 : 2;  // bytes per profile entry
-  const uint32_t baseA2 = lds0 + (slotA * kProfRows16 * RS + i * S) * EB;
-  const uint32_t baseB2 = lds0 + (slotB * kProfRows16 * RS + i * S) * EB;
+  const uint32_t SLOT = (UNIT ? kProfRows16 : ProfRows(a)) * RS;  // elements per profile slot
+  const uint32_t baseA2 = lds0 + (slotA * SLOT + i * S) * EB;
+  const uint32_t baseB2 = lds0 + (slotB * SLOT + i * S) * EB;
   const uint8_t *dbp = a.db - kDbFrontPad;
   const uint32_t back = kDbFrontPad + a.dblen;
   const uint32_t xA = (vA ? offA + kDbFrontPad : back) - i, xB = (vB ? offB + kDbFrontPad : back) - i;

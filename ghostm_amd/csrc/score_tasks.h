@@ -308,7 +308,7 @@ inline size_t BuildScorePairs(uint64_t cand_begin, uint64_t n, uint32_t q_first,
 }
 
 // Which K2 kernel runs a segment (ScoreKind) and its work list.
-enum ScoreKind { kScoreRows = 0, kScoreUnit = 1, kScorePairs = 2 };
+enum ScoreKind { kScoreRows = 0, kScoreUnit = 1, kScorePairs = 2, kScoreRowsSparse = 3 };
 // below this many candidates per query the pair-table kernel runs (cfg 2: ~9
 // per query, K2 5.1 -> 3.4 ms per step, profiles/r5d/; at cfg 3's 63 per query
 // it lost to the unit kernel, 14.8 -> 18.4 ms; GHOSTM_K2_PAIR_MAX overrides,
@@ -330,18 +330,38 @@ constexpr uint64_t kScorePairMax = 16;
 // `out` as uint32 entries. `out` has room for ScoreTaskBound(...) tasks and n
 // uint32 entries. pairs_ok = false (a launch with the re-score guard, which
 // only k_score16f implements) keeps the profile kernels.
+// Sparse segments run the 16-bit-row profile kernel at 16 rows per lane with
+// kScoreQmaxSparse profiles per block (kScoreRowsSparse, `sparse_per_block`
+// candidates per block; 0 = not available for this query width / DB): cfg 2 K2
+// 3.33-3.40 against 3.38-3.46 ms per step with k_score_pair, two boxes
+// (profiles/r6i/, profiles/r6j/: 7 profiles per block beat 6, 5, 4 — block fill
+// over occupancy). GHOSTM_K2_SPARSE=pair keeps k_score_pair (A/B), GHOSTM_K2=sparse
+// forces the rows kernel at any density.
+inline bool SparseRowsDefault() {
+  const char *e = getenv("GHOSTM_K2_SPARSE");
+  return !(e && strcmp(e, "pair") == 0);
+}
+
 inline size_t BuildTasks(bool swar, uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32_t q_end,
                          const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets,
                          uint32_t per_block, kern::ScoreTask *out, int *kind_out, bool pairs_ok = true,
-                         const HostParallelFn *par = nullptr) {
+                         const HostParallelFn *par = nullptr, uint32_t sparse_per_block = 0) {
   const char *k2 = getenv("GHOSTM_K2");
   const char *how = getenv("GHOSTM_K2_TASKS");
   const bool force_unit = k2 && strcmp(k2, "unit") == 0, force_rows = k2 && strcmp(k2, "swar16") == 0;
   const bool force_pair = k2 && strcmp(k2, "pair") == 0;
+  const bool force_sparse = k2 && strcmp(k2, "sparse") == 0 && sparse_per_block;
   bool unit = false, paired = false;
   const uint64_t per_query = n / std::max<uint32_t>(1, q_end - q_first);
   uint64_t pair_max = kScorePairMax;
   if (const char *e = getenv("GHOSTM_K2_PAIR_MAX")) pair_max = strtoull(e, nullptr, 10);
+  if (swar && q_end > q_first && (force_sparse || (!force_pair && sparse_per_block && pairs_ok && !force_unit &&
+                                                    !force_rows && !how && per_query < pair_max &&
+                                                    SparseRowsDefault()))) {
+    *kind_out = kScoreRowsSparse;
+    return BuildScoreTasks(cand_begin, n, q_first, q_end, counts, offsets, sparse_per_block, kern::SparseSlots(),
+                           out);
+  }
   if (swar && pairs_ok && q_end > q_first && !force_unit && !force_rows && !how &&
       (force_pair || per_query < pair_max)) {
     *kind_out = kScorePairs;

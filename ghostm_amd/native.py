@@ -83,6 +83,7 @@ class GhostmStats(ctypes.Structure):
         ("score_launches_pair", c_uint64),
         ("seed_table_full", c_uint64),
         ("seed_compact_redo", c_uint64),
+        ("score_launches_sparse", c_uint64),
     ]
 
     def as_dict(self) -> dict:

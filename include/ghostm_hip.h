@@ -220,6 +220,8 @@ typedef struct GhostmStats {
   uint64_t seed_table_full;         /* K1 queries whose LDS bin table reached its probe bound (redone by the
                                        table-free merge kernel) */
   uint64_t seed_compact_redo;       /* K1 compactions re-run by the host (queue overflow, candidate buffers grown) */
+  uint64_t score_launches_sparse;   /* K2 launches of sparse segments run by the 16-row profile kernel (k_score16f<16, true>,
+                                       seven query profiles per block) */
 } GhostmStats;
 
 /* Session: parse `aln` options exactly like the reference (getopt string

@@ -7,7 +7,7 @@ own code) and checks the golden variants under the kernel forms that read LDS:
 
   golden:  every golden variant with the default kernels, with the unit-pair
            K2 forced as paired and as consecutive tasks, and with the sparse
-           segments' pair-table K2 forced;
+           segments' pair-table and 16-row profile K2s forced;
   kernels: every K3 scan mode, every K4 mode, every K1 size class and the
            offset pass (class caps at the dataset's quartiles, slot cap 2), the
            bin table's probe bound lowered to 0 and 1 windows (the table-free
@@ -58,6 +58,7 @@ def plan(group):
             for tasks in ("paired", "consecutive"):
                 yield ds, var, opts, dict(env, GHOSTM_K2="unit", GHOSTM_K2_TASKS=tasks), f"unit_{tasks}"
             yield ds, var, opts, dict(env, GHOSTM_K2="pair"), "pair"
+            yield ds, var, opts, dict(env, GHOSTM_K2="sparse"), "sparse_rows"
         return
     scan_sets = [("syn_small", "default", []), ("syn_dna", "default", []), ("syn_chunks", "default", []),
                  ("protein_testset", "y2", ["-y", "2"]),

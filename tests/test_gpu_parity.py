@@ -77,6 +77,21 @@ def test_gpu_pair_k2_matches_reference_golden(ds, var, opts, env, dataset, golde
         assert st["score_launches_pair"] == st["score_launches"]
 
 
+@pytest.mark.parametrize("ds,var,opts,env", cases.VARIANTS, ids=[f"{v[0]}/{v[1]}" for v in cases.VARIANTS])
+def test_gpu_sparse_rows_k2_matches_reference_golden(ds, var, opts, env, dataset, golden, tmp_path):
+    """Every golden variant with the sparse segments' 16-row profile kernel forced
+    at any density (GHOSTM_K2=sparse: k_score16f<16, true> with seven 27-row query
+    profiles per block, kScoreRowsSparse): the same windows, ENDs, DB ends,
+    short queries and gap settings as the other K2 forms."""
+    d = dataset(ds)
+    text, st = _gpu_text(d, opts, dict(env, GHOSTM_K2="sparse"), str(tmp_path / "g.out"))
+    want = golden["aln"][f"{ds}/{var}"]
+    (tmp_path / "g.out").write_bytes(text)
+    assert cases.sha256(str(tmp_path / "g.out")) == want["sha256"]
+    if st["score_launches_swar"] == st["score_launches"] > 0:  # integer patterns fit: the sparse kernel ran
+        assert st["score_launches_sparse"] == st["score_launches"]
+
+
 @pytest.mark.parametrize("merge", ["device", "device_thread", "host"])
 @pytest.mark.parametrize("ds,var,opts,env", cases.BATCH_VARIANTS,
                          ids=[f"{v[0]}/{v[1]}" for v in cases.BATCH_VARIANTS])
