@@ -17,6 +17,7 @@
 #include <fstream>
 #include <iostream>
 #include <stdexcept>
+#include <thread>
 
 #include "common.h"
 #include "worker_pool.h"
@@ -700,15 +701,37 @@ void Session::Load(uint32_t shard_rank, uint32_t shard_world, bool local, std::v
   // are still being read (cfg3: the 34 MB DB and index upload took 1.5 ms of a
   // 4.1 ms session create after every read, profiles/r5ad/)
   std::mutex upload_mu;
+  // host copies resident on the device are dropped on a thread of their own
+  // after creation (unmapping ~40 MB of chunk files took ~0.3 ms per 12.7 MB
+  // on the critical path, and under the upload lock)
+  std::mutex drop_mu;
+  std::vector<std::shared_ptr<const void>> drop;
+  auto drop_later = [&](std::shared_ptr<const void> h) {
+    std::lock_guard<std::mutex> lock(drop_mu);
+    drop.push_back(std::move(h));
+  };
+  struct DropInBackground {
+    std::vector<std::shared_ptr<const void>> &d;
+    ~DropInBackground() {
+      if (d.empty()) return;
+      try {
+        std::thread([h = std::move(d)]() mutable { h.clear(); }).detach();
+      } catch (...) {
+        d.clear();  // no thread: drop them here
+      }
+    }
+  } drop_in_background{drop};
   auto upload_db = [&](DbData &d) {
-    std::lock_guard<std::mutex> lock(upload_mu);
-    const DbChunk &c = d.chunk;
-    d.dev = dev.UploadDb(c.seq.data(), c.len, c.keys_count.data(), c.kcl, c.positions.data(), c.npos);
-    if (c.nseq) dev.SetDbSubjects(d.dev, c.starts.data(), c.nseq);
+    {
+      std::lock_guard<std::mutex> lock(upload_mu);
+      const DbChunk &c = d.chunk;
+      d.dev = dev.UploadDb(c.seq.data(), c.len, c.keys_count.data(), c.kcl, c.positions.data(), c.npos);
+      if (c.nseq) dev.SetDbSubjects(d.dev, c.starts.data(), c.nseq);
+    }
     // resident on the device from here; the host keeps names and starts
-    d.chunk.seq.Release();
-    d.chunk.keys_count.Release();
-    d.chunk.positions.Release();
+    drop_later(d.chunk.seq.Detach());
+    drop_later(d.chunk.keys_count.Detach());
+    drop_later(d.chunk.positions.Detach());
   };
   auto upload_query = [&](QueryData &q) {
     std::lock_guard<std::mutex> lock(upload_mu);
@@ -835,7 +858,7 @@ void Session::Load(uint32_t shard_rank, uint32_t shard_world, bool local, std::v
 
   for (QueryData &q : queries_) {
     if (!q.dev) upload_query(q);  // (uploaded while reading when unsharded)
-    q.chunk.seq.Release();  // resident on the device (qlen and names stay on the host)
+    drop_later(q.chunk.seq.Detach());  // resident on the device (qlen and names stay on the host)
   }
   TraceMark("queries_released");
   // query chunks read past a missing one are not used (freed by `unadopted`)
@@ -1527,7 +1550,7 @@ void Session::FormatSelected(const QueryData &q, uint32_t g0, const std::vector<
   // timeline diagnostics: each worker's wall and on-CPU time (a thread that
   // waits for a CPU, e.g. under a cgroup quota, shows wall >> CPU)
   const bool trace = TraceOn();
-  std::vector<double> wall(trace ? workers : 0), cpu(trace ? workers : 0);
+  std::vector<double> wall(trace ? pieces : 0), cpu(trace ? pieces : 0);  // per piece
   ParallelForPieces(ng, pieces, workers, [&](size_t b, size_t e, unsigned t) {
     const double w0 = trace ? NowSeconds() : 0.0, c0 = trace ? ThreadCpuSeconds() : 0.0;
     struct Done {
@@ -1567,7 +1590,7 @@ void Session::FormatSelected(const QueryData &q, uint32_t g0, const std::vector<
   abandon.armed = false;
   if (trace) {
     double ws = 0, cs = 0, wm = 0;
-    for (unsigned t = 0; t < workers; ++t) ws += wall[t], cs += cpu[t], wm = std::max(wm, wall[t]);
+    for (size_t t = 0; t < pieces; ++t) ws += wall[t], cs += cpu[t], wm = std::max(wm, wall[t]);
     TraceMark("fmt_wall_max_us", (uint64_t)(wm * 1e6));
     TraceMark("fmt_wall_sum_us", (uint64_t)(ws * 1e6));
     TraceMark("fmt_cpu_sum_us", (uint64_t)(cs * 1e6));

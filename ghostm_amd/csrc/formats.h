@@ -65,6 +65,13 @@ class FileArray {
   bool Map(const std::string &path, uint64_t off, size_t n);
   void Own(std::vector<T> v);
   void Release() { *this = FileArray(); }
+  // empties the array and hands over what held its contents (the mapping or
+  // the owned vector), so the caller can drop it elsewhere
+  std::shared_ptr<const void> Detach() {
+    std::shared_ptr<const void> h = std::move(hold_);
+    *this = FileArray();
+    return h;
+  }
 
  private:
   const T *p_ = nullptr;

@@ -239,6 +239,26 @@ def test_streamed_output_file(merge, ds, var, opts, dataset, golden, tmp_path):
     assert _sha(text) == golden["aln"][f"{ds}/{var}"]["sha256"]
 
 
+def test_streamed_output_with_host_trace(dataset, golden, tmp_path):
+    """A streamed run with the host timeline on (GHOSTM_TRACE=1, read once per
+    process, so in a child process): the per-piece trace counters and the
+    writer's marks must not disturb the run, and the file is the reference's."""
+    import subprocess
+    import sys
+
+    d = dataset("syn_small")
+    out = tmp_path / "traced.out"
+    code = ("import sys; sys.path.insert(0, sys.argv[1]); from ghostm_amd.aligner import Session; "
+            "s = Session(['-i', sys.argv[2] + '/q', '-d', sys.argv[2] + '/db', '-o', sys.argv[3], '-D', '0']); "
+            "s.run(to_file=True); s.close()")
+    env = dict(os.environ, GHOSTM_TRACE="1", GHOSTM_SEGMENT_CANDS="300", GHOSTM_TAIL_CANDS="40")
+    r = subprocess.run([sys.executable, "-c", code, cases.REPO, d, str(out)], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "w_end" in r.stderr and "fmt_wall_max_us" in r.stderr
+    assert _sha(out.read_bytes()) == golden["aln"]["syn_small/default"]["sha256"]
+
+
 def test_streamed_output_unwritable_path(dataset, tmp_path):
     """As the reference's unchecked ofstream: an -o path that cannot be opened
     writes nothing and the run still succeeds."""

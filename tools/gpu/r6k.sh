@@ -1,0 +1,13 @@
+# round 6 k: cfg3/cfg2 end-to-end host timelines with the create-path marks
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r6k
+mkdir -p $O
+cd $R
+timeout -k 10 300 python -u -m pytest tests/test_gpu_scale.py -m gpu -x -q --timeout 120 --timeout-method thread -k streamed > $O/tests.log 2>&1 || { echo "tests failed"; tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+for p in cfg3 cfg2; do
+  GHOSTM_TRACE=1 timeout -k 10 300 python3 -u tools/e2e_trace.py --preset $p --runs 5 --workdir /tmp/r6k_$p > $O/e2e_$p.txt 2> $O/e2e_${p}_trace.log || { echo "$p failed"; tail -5 $O/e2e_${p}_trace.log; exit 1; }
+  cat $O/e2e_$p.txt
+done
+echo done
