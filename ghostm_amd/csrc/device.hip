@@ -1535,9 +1535,13 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
     const uint32_t ps = std::max<uint32_t>(pair_span, 1);
     const uint32_t runs_per_span = (ps + kern::kPairRun - 1) / kern::kPairRun;
     const uint64_t runs = (uint64_t)((n + ps - 1) / ps) * runs_per_span;
+    // (diagnostics: GHOSTM_K3_SCAN_ORDER=query runs the scan's pairs in query
+    // order, as a per-query-profile scan would have to, instead of by width)
+    const char *order_env = getenv("GHOSTM_K3_SCAN_ORDER");
+    const bool query_order = order_env && strcmp(order_env, "query") == 0;
     hipLaunchKernelGGL(kern::k_tb_pairs, dim3((uint32_t)((runs + 255) / 256)), b256, 0, S(stream_), a.qid,
                        I.tb_width.as<uint32_t>(), n, ps, I.tb_pair_a.as<uint32_t>(), I.tb_pair_b.as<uint32_t>(),
-                       I.tb_key.as<uint32_t>(), hist1);
+                       I.tb_key.as<uint32_t>(), hist1, query_order);
     const dim3 gsort((n + kern::kCsortTile - 1) / kern::kCsortTile);
     hipLaunchKernelGGL(kern::k_csort_scatter, gsort, b256, 0, S(stream_), I.tb_key.as<uint32_t>(), n, true,
                        hist1, cur1, I.tb_order1.as<uint32_t>());
@@ -1579,6 +1583,7 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
     sa.base = a.base;
     sa.items = I.tb_order1.as<uint32_t>();
     sa.item_total = hist1 + NB;
+    sa.query_order = query_order ? 1u : 0u;
     sa.open = a.open;
     sa.ext = a.ext;
     sa.ncols = I.tb_ncols.as<uint32_t>();

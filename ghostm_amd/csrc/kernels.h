@@ -3541,9 +3541,11 @@ __global__ __launch_bounds__(256) void k_tb_prep(const uint32_t *qid, const uint
 // longer window, counted into hist[key] and hist[kSortBins] (total); unused
 // item positions get key 0.
 constexpr uint32_t kPairRun = 32;  // longer runs are paired 32 slots at a time
+// (key_one, diagnostics GHOSTM_K3_SCAN_ORDER=query: every item gets key 1, so the
+// scan runs the pairs in query order, not by width)
 __global__ __launch_bounds__(256) void k_tb_pairs(const uint32_t *qid, const uint32_t *width, uint32_t n,
                                                   uint32_t span, uint32_t *pair_a, uint32_t *pair_b,
-                                                  uint32_t *key, uint32_t *hist) {
+                                                  uint32_t *key, uint32_t *hist, bool key_one = false) {
   GHOSTM_POISON_LDS();
   __shared__ uint32_t s_hist[kSortBins];
   __shared__ uint32_t s_total;
@@ -3583,7 +3585,7 @@ __global__ __launch_bounds__(256) void k_tb_pairs(const uint32_t *qid, const uin
       } else {
         k += 1;
       }
-      const uint32_t kk = min(max(wa, wb), kSortBins - 1);
+      const uint32_t kk = key_one ? 1u : min(max(wa, wb), kSortBins - 1);
       pair_a[first + items] = a;
       pair_b[first + items] = b;
       key[first + items] = kk;
@@ -3703,6 +3705,7 @@ struct TbScanArgs {
   uint32_t *skey;
   uint32_t strips;
   uint32_t strip_shift;        // the key DP's strip = the scan's strip >> strip_shift (scan G = key G << shift)
+  uint32_t query_order;        // items in query order (k_tb_pairs key_one): the wave's longest window by a wave max
 };
 
 // The scan keeps each row's table offset in its own register: a VOP2 address
@@ -3869,6 +3872,7 @@ __global__ __launch_bounds__(kScanBlock) void k_tb_scan(TbScanArgs a) {
     const uint32_t last = a.items[hi - 1];
     uint32_t wmax = __builtin_amdgcn_readfirstlane(a.key[last]);  // key of an item index
     if (wmax >= kSortBins - 1) wmax = a.base;
+    if (a.query_order) wmax = __builtin_amdgcn_readfirstlane(WaveMax(max(wA, wB)));
     const uint32_t steps = wmax + a.G - 1;
     // residues of the reverse window, two columns ahead. General steps: outside
     // the window (fill: j < 0, beyond: its end or the subject's start) a column
