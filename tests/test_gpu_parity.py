@@ -63,9 +63,10 @@ def test_gpu_unit_k2_matches_reference_golden(ds, var, opts, env, tasks, dataset
 
 @pytest.mark.parametrize("ds,var,opts,env", cases.VARIANTS, ids=[f"{v[0]}/{v[1]}" for v in cases.VARIANTS])
 def test_gpu_pair_k2_matches_reference_golden(ds, var, opts, env, dataset, golden, tmp_path):
-    """Every golden variant with the sparse segments' K2 forced at any density
-    (GHOSTM_K2=pair: k_score_pair, the pair-table kernel that runs segments of
-    fewer than 24 candidates per query by default): windows over one or several
+    """Every golden variant with the pair-table K2 forced at any density
+    (GHOSTM_K2=pair: k_score_pair; by default sparse segments, fewer than
+    kScorePairMax = 16 candidates per query, run the sparse rows kernel and
+    GHOSTM_K2_SPARSE=pair selects this one): windows over one or several
     subject ENDs, a window starting at an END, the DB's end, one-subject DBs,
     S = 16 and 8, G = 1, odd candidate counts (single pairs), every gap setting."""
     d = dataset(ds)
