@@ -175,6 +175,36 @@ inline size_t CountScoreTasks(uint64_t cand_begin, uint64_t n, uint32_t q_first,
   return nt + (open_task && cur ? 1 : 0);
 }
 
+// BuildScoreTasks in parts on host threads: the query range is cut into parts,
+// each part's tasks counted (CountScoreTasks), then written at the part's
+// prefix. A task never spans two parts (a part starts a fresh task), which
+// changes only how candidates are grouped into blocks, never a score; at most
+// one task more per part, inside ScoreTaskBound's one-per-query slack. A
+// chunk's first segment builds its tasks while the GPU waits (125 K-query shard:
+// 74 K tasks, 0.34 ms on one thread, profiles/r5ap/). GHOSTM_K2_TASKS_PAR=0 keeps
+// one thread (A/B).
+inline size_t BuildScoreTasksParallel(uint64_t cand_begin, uint64_t n, uint32_t q_first, uint32_t q_end,
+                                      const std::vector<uint32_t> &counts, const std::vector<uint64_t> &offsets,
+                                      uint32_t per_block, uint32_t qmax, kern::ScoreTask *out,
+                                      const HostParallelFn *par) {
+  constexpr uint32_t kPartQueries = 4096;
+  const uint32_t nqr = q_end > q_first ? q_end - q_first : 0;
+  const char *e = getenv("GHOSTM_K2_TASKS_PAR");
+  if (!par || !*par || nqr < 2 * kPartQueries || (e && strcmp(e, "0") == 0))
+    return BuildScoreTasks(cand_begin, n, q_first, q_end, counts, offsets, per_block, qmax, out);
+  const size_t parts = std::min<size_t>(16, nqr / kPartQueries);
+  auto cut = [&](size_t k) { return q_first + (uint32_t)((uint64_t)nqr * k / parts); };
+  std::vector<size_t> at(parts + 1, 0);
+  (*par)(parts, [&](size_t k) {
+    at[k + 1] = CountScoreTasks(cand_begin, n, cut(k), cut(k + 1), counts, offsets, per_block, qmax);
+  });
+  for (size_t k = 0; k < parts; ++k) at[k + 1] += at[k];
+  (*par)(parts, [&](size_t k) {
+    BuildScoreTasks(cand_begin, n, cut(k), cut(k + 1), counts, offsets, per_block, qmax, out + at[k]);
+  });
+  return at[parts];
+}
+
 // The blocks BuildScoreTasksPaired would make, from a histogram of the
 // remainders (no tasks built).
 // Blocks the pairing makes from a histogram of remainder sizes (rem[r] =
@@ -359,8 +389,8 @@ inline size_t BuildTasks(bool swar, uint64_t cand_begin, uint64_t n, uint32_t q_
                                                     !force_rows && !how && per_query < pair_max &&
                                                     SparseRowsDefault()))) {
     *kind_out = kScoreRowsSparse;
-    return BuildScoreTasks(cand_begin, n, q_first, q_end, counts, offsets, sparse_per_block, kern::SparseSlots(),
-                           out);
+    return BuildScoreTasksParallel(cand_begin, n, q_first, q_end, counts, offsets, sparse_per_block,
+                                   kern::SparseSlots(), out, par);
   }
   if (swar && pairs_ok && q_end > q_first && !force_unit && !force_rows && !how &&
       (force_pair || per_query < pair_max)) {
@@ -383,8 +413,8 @@ inline size_t BuildTasks(bool swar, uint64_t cand_begin, uint64_t n, uint32_t q_
   }
   *kind_out = unit ? kScoreUnit : kScoreRows;
   if (unit && paired) return BuildScoreTasksPaired(cand_begin, n, q_first, q_end, counts, offsets, per_block, out);
-  return BuildScoreTasks(cand_begin, n, q_first, q_end, counts, offsets, per_block,
-                         unit ? kern::kScoreQmaxUnit : kern::kScoreQmax, out);
+  return BuildScoreTasksParallel(cand_begin, n, q_first, q_end, counts, offsets, per_block,
+                                 unit ? kern::kScoreQmaxUnit : kern::kScoreQmax, out, par);
 }
 
 }  // namespace ghostm

@@ -192,6 +192,32 @@ int main() {
       printf("parallel pair list differs (%zu against %zu pairs, %u queries)\n", n2, n1, q1 - q0);
       return 1;
     }
+    // consecutive tasks built in parts on threads (a part starts a fresh task):
+    // every candidate once, every task within per_block and qmax, inside the
+    // bound; two and four queries per block, and the sparse kernel's seven
+    std::vector<uint32_t> qid_of(total);
+    for (uint32_t q = 0; q < nq; ++q)
+      for (uint32_t c = 0; c < counts[q]; ++c) qid_of[offsets[q] + c] = q;
+    for (uint32_t qmax : {2u, 4u, 7u}) {
+      const uint32_t pb = qmax == 7 ? 64u : per_block;
+      std::vector<ScoreTask> tasks(ghostm::ScoreTaskBound(e - b, q0, q1, pb, qmax));
+      const size_t nt = ghostm::BuildScoreTasksParallel(b, e - b, q0, q1, counts, offsets, pb, qmax, tasks.data(), &par);
+      if (nt > tasks.size()) { printf("parallel tasks over the bound\n"); return 1; }
+      if (Check("consecutive in parts", tasks, nt, qmax == 2, qmax, b, e - b, qid_of, pb)) return 1;
+    }
+    // the chosen kernel with the sparse rows kernel available: below
+    // kScorePairMax per query it takes seven-profile tasks of 64 candidates
+    {
+      std::vector<ScoreTask> tasks(std::max<size_t>(ghostm::ScoreTaskBound(e - b, q0, q1, 64, 7),
+                                                    (e - b) * 4 / sizeof(ScoreTask) + 1));
+      int kind = -1;
+      const size_t nt = ghostm::BuildTasks(true, b, e - b, q0, q1, counts, offsets, per_block, tasks.data(), &kind,
+                                           true, &par, 64);
+      if ((e - b) / std::max<uint32_t>(1, q1 - q0) < ghostm::kScorePairMax) {
+        if (kind != ghostm::kScoreRowsSparse) { printf("sparse segment without the sparse kernel\n"); return 1; }
+        if (Check("sparse rows", tasks, nt, false, 7, b, e - b, qid_of, 64)) return 1;
+      }
+    }
     ++trials;
   }
   printf("%llu trials ok; waves: paired %llu, consecutive %llu\n", (unsigned long long)trials,
