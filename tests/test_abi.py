@@ -94,3 +94,19 @@ def test_library_source_hash_matches_tree(built):
     from conftest import library_hash_mismatch
 
     assert library_hash_mismatch() is None
+
+
+def test_source_hash_covers_the_native_sources(tmp_path):
+    """ghostm_amd/srchash.py hashes every csrc source and the header by name and
+    content (the Makefile compiles the same hash into GhostmBuildInfo), and
+    info_hash reads it back from a build-info string."""
+    from ghostm_amd import srchash
+
+    files = [os.path.relpath(p, srchash.REPO_DIR) for p in srchash.source_files()]
+    assert "include/ghostm_hip.h" in files
+    for name in ("kernels.h", "device.hip", "aligner.cpp", "Makefile"):
+        assert os.path.join("ghostm_amd", "csrc", name) in files
+    h = srchash.tree_hash()
+    assert len(h) == 16 and int(h, 16) >= 0
+    assert srchash.info_hash(f"ghostm_hip gfx950: K1 ...; LDS poison build; src {h}") == h
+    assert srchash.info_hash("ghostm_hip gfx950: K1 ...") is None
