@@ -1650,11 +1650,20 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
   // the (at most kTbStripClasses) extra waves
   const dim3 grid((n + per_block - 1) / per_block + (a.class_off ? 1 : 0)), block(kern::kTbBlock);
   const bool fin = a.best_h != nullptr;  // the scan's maxima: no running maximum in the key DP
-#define GHOSTM_TB(SS)                                                                                              \
-  if (key16 && fin) hipLaunchKernelGGL((kern::k_traceback_key<SS, 16, true>), grid, block, 0, S(stream_), a);      \
-  else if (key16) hipLaunchKernelGGL((kern::k_traceback_key<SS, 16, false>), grid, block, 0, S(stream_), a);       \
-  else if (key17 && fin) hipLaunchKernelGGL((kern::k_traceback_key<SS, 17, true>), grid, block, 0, S(stream_), a); \
-  else if (key17) hipLaunchKernelGGL((kern::k_traceback_key<SS, 17, false>), grid, block, 0, S(stream_), a);       \
+  // the framed key DP (kernels.h k_traceback_key FRAME): h + every column's
+  // frame, (span + 1) * ext_pen, must still fit the field; GHOSTM_K3_KEYFRAME=0
+  // keeps the unframed one
+  const char *kf_env = getenv("GHOSTM_K3_KEYFRAME");
+  const int64_t kframe = hmax + (int64_t)(span + 1) * (-(int64_t)a.ext);
+  const bool frame = fin && !(kf_env && strcmp(kf_env, "0") == 0) && (key16 ? kframe < 8000 : kframe < 4000);
+#define GHOSTM_TB(SS)                                                                                                 \
+  if (key16 && frame) hipLaunchKernelGGL((kern::k_traceback_key<SS, 16, true, true>), grid, block, 0, S(stream_), a); \
+  else if (key16 && fin) hipLaunchKernelGGL((kern::k_traceback_key<SS, 16, true>), grid, block, 0, S(stream_), a);    \
+  else if (key16) hipLaunchKernelGGL((kern::k_traceback_key<SS, 16, false>), grid, block, 0, S(stream_), a);          \
+  else if (key17 && frame)                                                                                            \
+    hipLaunchKernelGGL((kern::k_traceback_key<SS, 17, true, true>), grid, block, 0, S(stream_), a);                   \
+  else if (key17 && fin) hipLaunchKernelGGL((kern::k_traceback_key<SS, 17, true>), grid, block, 0, S(stream_), a);    \
+  else if (key17) hipLaunchKernelGGL((kern::k_traceback_key<SS, 17, false>), grid, block, 0, S(stream_), a);          \
   else hipLaunchKernelGGL(kern::k_traceback<SS>, grid, block, 0, S(stream_), a);
   switch (lay.S) {
     case 32: GHOSTM_TB(32); break;
@@ -1665,6 +1674,7 @@ void DeviceModule::LaunchTraceback(kern::TbArgs a, DevQuery *q, uint32_t n, cons
   HIP_CHECK(hipGetLastError());
   times_.traceback_launches += 1;
   times_.traceback_launches_key += key ? 1 : 0;
+  times_.traceback_launches_keyframe += key && frame ? 1 : 0;
 }
 
 void DeviceModule::ResetCarry(DevQuery *q, uint32_t cap) {

@@ -2833,14 +2833,28 @@ __device__ inline uint32_t Bfi(uint32_t m, uint32_t x, uint32_t y) {
 
 __device__ inline int ShiftUpI(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xF, 0xF, false); }
 
-template <int S, int MLW, bool FINAL>
+// FRAME (FINAL only, round 6): every key of column j is stored with FR_j =
+// j * (-ext) added to its h field, as K2's column frame, so E's extension needs
+// no add: E'(j) = max3(A', Bfi(HIGH, E'(j-1), A'), zero'(j)) with A' = K'(j-1) +
+// open - ext, and the diagonal's -ext step sits in the table (T - EXTK). The
+// zero floor moves from F to E (zero'(j) = the zero key + FR_j, one register per
+// column): E and F agree with the unframed chains at every h >= 0, values below
+// 0 never rise above 0 again through an extension, and the cell maximum still
+// sees the zero key, so every key compared (and the result) is unchanged. 11
+// VALU instructions per cell instead of 12. The host uses it while hmax + the
+// largest frame fits the h field.
+template <int S, int MLW, bool FINAL, bool FRAME = false>
 __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
   GHOSTM_POISON_LDS();
+  static_assert(!FRAME || FINAL, "the frame changes h across columns: no running maximum");
   using KL = KeyLayout<MLW>;
   // rows of 33 dwords: lanes reading the same query code for different DB codes
   // fall on different banks
   __shared__ int s_key[32 * 33];
-  for (uint32_t e = threadIdx.x; e < 32 * 32; e += kTbBlock) s_key[(e >> 5) * 33 + (e & 31)] = a.mat_tb[e];
+  {
+    const int tstep = FRAME ? (int)((uint32_t)a.ext << KL::kHS) : 0;  // the diagonal's frame step
+    for (uint32_t e = threadIdx.x; e < 32 * 32; e += kTbBlock) s_key[(e >> 5) * 33 + (e & 31)] = a.mat_tb[e] - tstep;
+  }
   __syncthreads();
 
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -2914,24 +2928,30 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
       }
     }
   }
-  int K[S], KE[S];
-#pragma unroll
-  for (int u = 0; u < S; ++u) { K[u] = 0; KE[u] = 0; }
-  int bestK = 0, best_col = 0;
-  int kout = 0, kfout = 0, kprev = 0;
-  bool done = false;
-  uint32_t ncols = 0;
   const int OPENK = (int)(((uint32_t)a.open << KL::kHS) | (1u << MLW) | 0x80u);  // E: prio 1, len + 1
   const int OPENKF = (int)(((uint32_t)a.open << KL::kHS) | 0x80u);              // F: prio 0, len + 1
   const int EXTK = (int)((uint32_t)a.ext << KL::kHS);
   const int KZ = (int)(3u << MLW);
   const uint32_t HIGH = ~KL::kLow;
+  // FRAME: fr = FR_j of this lane's column j = step - i (real 0 there); the
+  // state before column 0 is real 0 in column -1's frame (EXTK), as is what an
+  // idle lane hands down
+  const int OPENKE = FRAME ? OPENK - EXTK : OPENK;
+  int fr = FRAME ? (int)i * EXTK : 0;
+  int K[S], KE[S];
+#pragma unroll
+  for (int u = 0; u < S; ++u) { K[u] = FRAME ? EXTK : 0; KE[u] = FRAME ? EXTK : 0; }
+  int bestK = 0, best_col = 0;
+  // what this lane hands down before step 0: its column -i - 1
+  int kout = FRAME ? fr + EXTK : 0, kfout = kout, kprev = FRAME ? EXTK : 0;
+  bool done = false;
+  uint32_t ncols = 0;
   int j = -(int)i;
   const uint32_t wmax = WaveMax(valid ? width : 0u);
   const uint32_t steps = wmax ? wmax + G - 1 : 0u;
   for (uint32_t step = 0; step < steps; ++step, ++j) {
     int kin = ShiftUpI(kout), kfin = ShiftUpI(kfout);
-    if (i == 0) { kin = 0; kfin = 0; }
+    if (i == 0) { kin = fr; kfin = fr; }
     const int kdiag0 = kprev;
     kprev = kin;
     bool active = valid && !done && j >= 0 && (uint32_t)j < width;
@@ -2944,6 +2964,7 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
       const char *rowp = reinterpret_cast<const char *>(s_key) + MulU24(c, 33 * 4);
       auto T = [&](int u) { return *reinterpret_cast<const int *>(rowp + ((qoff[u >> 2] >> (8 * (u & 3))) & 0xFFu)); };
       int sd = kdiag0 + T(0), KF = kfin, kup = kin;
+      const int kz = KZ + fr;  // FRAME: the zero key of this column
 #pragma unroll
       for (int k = 0; k < S; k += 4) {
         // diagonal sums of the chunk (and of the next chunk's first row) from the
@@ -2957,16 +2978,23 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
           const int u = k + v;
-          const int A = K[u] + OPENK;
-          const int B = (int)Bfi(HIGH, (uint32_t)(KE[u] + EXTK), (uint32_t)A);
-          KE[u] = max(A, B);
+          const int A = K[u] + OPENKE;
           const int AF = kup + OPENKF;
           const int BF = (int)Bfi(HIGH, (uint32_t)(KF + EXTK), (uint32_t)AF);
-          // F floored at the zero key: only values <= 0 change, and those never
-          // beat the zero key (prio 3) nor feed a positive F further down (a
-          // floor extended is ext < 0), so the cell maximum needs no separate
-          // max with the zero key
-          KF = max(max(AF, BF), KZ);
+          if constexpr (FRAME) {
+            // E extended in the frame (no add), floored at this column's zero key
+            const int B = (int)Bfi(HIGH, (uint32_t)KE[u], (uint32_t)A);
+            KE[u] = max(max(A, B), kz);
+            KF = max(AF, BF);
+          } else {
+            const int B = (int)Bfi(HIGH, (uint32_t)(KE[u] + EXTK), (uint32_t)A);
+            KE[u] = max(A, B);
+            // F floored at the zero key: only values <= 0 change, and those never
+            // beat the zero key (prio 3) nor feed a positive F further down (a
+            // floor extended is ext < 0), so the cell maximum needs no separate
+            // max with the zero key
+            KF = max(max(AF, BF), KZ);
+          }
           const int kc = (int)((uint32_t)max(max(ks[v], KE[u]), KF) & ~KL::kPrio);
           K[u] = kc;
           kup = kc;
@@ -2985,9 +3013,10 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
       kfout = KF;
       ++ncols;
     } else {
-      kout = 0;
-      kfout = 0;
+      kout = fr;
+      kfout = fr;
     }
+    if constexpr (FRAME) fr -= EXTK;
   }
   int C, ML;
   if constexpr (FINAL) {
@@ -2996,11 +3025,13 @@ __global__ __launch_bounds__(kTbBlock) void k_traceback_key(TbArgs a) {
     // lanes, then rows) there whose h equals it. A maximum of 0 keeps the
     // reference's initial j* = 0 and empty (len, match).
     const uint32_t bh = valid ? a.best_h[hit] : 0u;
+    // FRAME: K is in column width - 1's frame
+    const uint32_t bhf = FRAME ? bh + (width - 1) * (uint32_t)(-a.ext) : bh;
     int found = 0, fml = 0;
     if (bh) {
 #pragma unroll
       for (int u = S - 1; u >= 0; --u)
-        if (((uint32_t)K[u] >> KL::kHS) == bh) { found = 1; fml = (int)((uint32_t)K[u] & KL::kMl); }
+        if (((uint32_t)K[u] >> KL::kHS) == bhf) { found = 1; fml = (int)((uint32_t)K[u] & KL::kMl); }
     }
     for (uint32_t k = 1; k < G; ++k) {
       const int src = (int)(g * G + k);

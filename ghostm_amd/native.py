@@ -84,6 +84,7 @@ class GhostmStats(ctypes.Structure):
         ("seed_table_full", c_uint64),
         ("seed_compact_redo", c_uint64),
         ("score_launches_sparse", c_uint64),
+        ("traceback_launches_keyframe", c_uint64),
     ]
 
     def as_dict(self) -> dict:

@@ -222,6 +222,7 @@ typedef struct GhostmStats {
   uint64_t seed_compact_redo;       /* K1 compactions re-run by the host (queue overflow, candidate buffers grown) */
   uint64_t score_launches_sparse;   /* K2 launches of sparse segments run by the 16-row profile kernel (k_score16f<16, true>,
                                        seven query profiles per block) */
+  uint64_t traceback_launches_keyframe; /* K3 key DPs run with the column-framed E chain (k_traceback_key FRAME) */
 } GhostmStats;
 
 /* Session: parse `aln` options exactly like the reference (getopt string

@@ -370,7 +370,7 @@ def test_wide_band_traceback_uses_key_kernel(dataset, golden, tmp_path):
     assert st["traceback_launches_key"] == st["traceback_launches"] > 0
 
 
-@pytest.mark.parametrize("mode", ["default", "priv", "f16frame", "f16plain", "int16", "0"])
+@pytest.mark.parametrize("mode", ["default", "priv", "f16frame", "f16plain", "int16", "0", "keyframe0"])
 @pytest.mark.parametrize("ds,var,opts", [("syn_small", "default", []), ("syn_dna", "default", []),
                                          ("syn_chunks", "default", []), ("protein_testset", "y2", ["-y", "2"]),
                                          ("syn_small", "r64_pam250", ["-r", "64", "-M", cases.PAM250, "-y", "2"])])
@@ -379,18 +379,22 @@ def test_traceback_scan_modes_match_golden(mode, ds, var, opts, dataset, golden,
     0..j* in j*-sorted order) in its encodings (default: the column-framed scan
     over 16-bit integer patterns; priv: the same scan reading a bank-private
     unit-word table; f16frame, f16plain, int16), and the single-pass traceback
-    (GHOSTM_K3_SCAN=0): each reproduces the golden output."""
+    (GHOSTM_K3_SCAN=0): each reproduces the golden output. After a scan the key
+    DP runs with its column-framed E chain (k_traceback_key FRAME);
+    keyframe0 (GHOSTM_K3_KEYFRAME=0) keeps the unframed one."""
     d = dataset(ds)
-    env = {} if mode == "default" else {"GHOSTM_K3_SCAN": mode}
+    env = ({} if mode == "default" else {"GHOSTM_K3_KEYFRAME": "0"} if mode == "keyframe0"
+           else {"GHOSTM_K3_SCAN": mode})
     text, st = _gpu_text(d, opts, env, str(tmp_path / "g.out"))
     (tmp_path / "g.out").write_bytes(text)
     assert cases.sha256(str(tmp_path / "g.out")) == golden["aln"][f"{ds}/{var}"]["sha256"]
     assert st["traceback_launches"] > 0
+    assert st["traceback_launches_keyframe"] == (0 if mode in ("0", "keyframe0") else st["traceback_launches"])
     if mode == "0":
         assert st["traceback_launches_scan"] == 0 and st["traceback_scan_cells"] == 0
     else:
         # default: the framed scan over 16-bit integer patterns; the others not
-        swar = mode in ("default", "priv")
+        swar = mode in ("default", "priv", "keyframe0")
         assert st["traceback_launches_scan_swar"] == (st["traceback_launches"] if swar else 0)
         assert st["traceback_launches_scan"] == st["traceback_launches"]
         assert st["traceback_scan_cells"] > 0
