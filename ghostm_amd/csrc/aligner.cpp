@@ -1695,6 +1695,7 @@ void Session::Run(bool stream_to_file) {
   stats_.seed_compact_redo = dt.seed_compact_redo;
   stats_.score_launches_sparse = dt.score_launches_sparse;
   stats_.traceback_launches_keyframe = dt.traceback_launches_keyframe;
+  stats_.score_launches_levels = dt.score_launches_levels;
   stats_.score_launches_swar = dt.score_launches_swar;
   stats_.score_launches_unit = dt.score_launches_unit;
   stats_.score_launches_pair = dt.score_launches_pair;

@@ -87,6 +87,7 @@ struct DeviceTimes {
   uint64_t score_launches_pair = 0;  // sparse segments: the pair-table kernel (k_score_pair)
   uint64_t seed_compact_redo = 0;    // K1 compactions re-run by the host (overflow, buffer growth)
   uint64_t seed_filter_overflows = 0;             // ... queries redone by k_seed_hash (queue overflow)
+  uint64_t score_launches_levels = 0;             // K2 launches with restart levels (k_score16f<S, true, false, true>)
   uint64_t traceback_launches_keyframe = 0;       // K3 key DPs with the column-framed E chain (k_traceback_key FRAME)
   uint64_t score_launches_sparse = 0;             // K2 launches of sparse segments run by k_score16f<16, true> (kScoreRowsSparse)
   uint64_t seed_table_full = 0;                   // ... queries redone by k_seed (bin table probe bound reached)

@@ -216,6 +216,7 @@ struct DevDb {
   DevBuf low;                      // kern::k_low_keys' bitmap
   uint32_t len = 0, kcl = 0, npos = 0;
   bool codes_le26 = false;         // every residue code <= 26 (the sparse K2 profiles hold rows 0..26)
+  uint32_t end_gap = UINT32_MAX;   // fewest positions from one END to the next (K2 restart levels)
   const uint8_t *Residues() const { return seq.as<uint8_t>() + kDbFront; }
   DevBuf subj;                     // subject starts (device merge)
   DevBuf subj_bucket;              // kern::SubjectOfBucketed's table
@@ -413,9 +414,10 @@ void DeviceModule::Bind(int device) {
   HIP_CHECK(hipFuncSetAttribute((const void *)GHOSTM_FILTER2, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)kFilterLds2));
   // the sparse rows K2 (kScoreRowsSparse): seven 27-row profiles, ~53 KB at L = 127
-  HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_score16f<16, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)(kern::kScoreQmaxSparse * kern::kProfRowsSparse * ((kMaxQueryLength + 15) / 16 * 16 + 8) * 2 +
-                                      32 * 32 * 2)));
+  for (const void *f : {(const void *)kern::k_score16f<16, true>, (const void *)kern::k_score16f<16, true, false, true>})
+    HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)(kern::kScoreQmaxSparse * kern::kProfRowsSparse * ((kMaxQueryLength + 15) / 16 * 16 + 8) * 2 +
+                                        32 * 32 * 2)));
   const int scan_lds = (int)kScanLds;
 #define GHOSTM_SCAN_ATTR(SS, HH, EE, FF)                                             \
   HIP_CHECK(hipFuncSetAttribute((const void *)kern::k_tb_scan<SS, HH, EE, FF>,       \
@@ -570,7 +572,16 @@ DevDb *DeviceModule::UploadDb(const uint8_t *seq, uint32_t len, const uint32_t *
     }
     if (hi & 0xE0E0E0E0E0E0E0E0ull) throw Error("database residue code out of range");
   }
+  // the closest two ENDs (subject boundaries): bounds the ENDs a K2 window can
+  // meet, which the restart-level kernel needs below the f16 infinity pattern
+  uint32_t end_gap = UINT32_MAX;
+  for (const uint8_t *p = seq, *last = nullptr, *e = seq + len;
+       (p = static_cast<const uint8_t *>(std::memchr(p, (int)kern::kSeqEnd, (size_t)(e - p)))) != nullptr; ++p) {
+    if (last) end_gap = std::min<uint32_t>(end_gap, (uint32_t)(p - last));
+    last = p;
+  }
   DevDb *d = new DevDb();
+  d->end_gap = end_gap;
   d->codes_le26 = (over26 & 0x8080808080808080ull) == 0;
   d->len = len;
   d->kcl = kcl;
@@ -1173,6 +1184,16 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
   const int64_t swar_restart = swar_low + sigma_max + bound + 32;
   const int64_t swar_top = swar_restart + sigma_max + bound + std::abs((int64_t)gap.open - gap.ext) + 32;
   const bool swar = framed && swar_top < 0x7C00 && !(force && strcmp(force, "f16frame") == 0);
+  // restart levels (k_score16f<S, true, false, true>): the k-th END of a window
+  // restarts at swar_restart + (k - 1) * step, step above the largest rise after
+  // a restart; the window's most ENDs (from the DB's closest two) must fit below
+  // f16 infinity. GHOSTM_K2_LEVELS=0 keeps the second END's reset.
+  const int64_t swar_rise = swar_top - swar_restart;
+  const int64_t swar_step = swar_rise + 32;
+  const uint64_t max_ends = d->end_gap == UINT32_MAX || base == 0 ? 1 : (uint64_t)(base - 1) / d->end_gap + 1;
+  const int64_t swar_cap = swar_restart + (int64_t)(max_ends - 1) * swar_step;
+  const char *levels_env = getenv("GHOSTM_K2_LEVELS");
+  const bool levels = swar && !(levels_env && strcmp(levels_env, "0") == 0) && max_ends <= 64 && swar_cap + swar_rise < 0x7C00;
   // framed: values stay exact and the -2040-based frame stays below the
   // post-END one while best + sigma_max < 2040; beyond, the guard flags them
   int guard = swar ? 0 : framed ? (bound + sigma_max < 2040 ? 0 : (int)(2040 - sigma_max)) : (bound < 2048 ? 0 : 2000);
@@ -1261,6 +1282,8 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
   a.out_base = cand_begin;
   a.swar_low = (uint32_t)swar_low;
   a.swar_restart = (uint32_t)swar_restart;
+  a.swar_step = levels ? (uint32_t)swar_step : 0u;
+  a.swar_cap = levels ? (uint32_t)swar_cap : 0u;
   if (pairs) {
     a.pairs = I.task_buf[buf].as<uint32_t>();
     a.npairs = (uint32_t)ntasks;
@@ -1315,11 +1338,13 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
       default: hipLaunchKernelGGL((kern::k_score_pair<8>), pgrid, pblock, plds, S(stream_), a); break;
     }
   } else if (sparse) {
-    hipLaunchKernelGGL((kern::k_score16f<16, true>), grid, block, lds, S(stream_), a);
+    if (levels) hipLaunchKernelGGL((kern::k_score16f<16, true, false, true>), grid, block, lds, S(stream_), a);
+    else hipLaunchKernelGGL((kern::k_score16f<16, true>), grid, block, lds, S(stream_), a);
   } else if (packed) {
     switch (lay.S) {
       case 32:
         if (unit) hipLaunchKernelGGL((kern::k_score16f<32, true, true>), grid, block, lds, S(stream_), a);
+        else if (levels) hipLaunchKernelGGL((kern::k_score16f<32, true, false, true>), grid, block, lds, S(stream_), a);
         else if (swar) hipLaunchKernelGGL((kern::k_score16f<32, true>), grid, block, lds, S(stream_), a);
         else if (framed) hipLaunchKernelGGL((kern::k_score16f<32>), grid, block, lds, S(stream_), a);
         else if (half) hipLaunchKernelGGL((kern::k_score16<32, true>), grid, block, lds, S(stream_), a);
@@ -1327,6 +1352,7 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
         break;
       case 16:
         if (unit) hipLaunchKernelGGL((kern::k_score16f<16, true, true>), grid, block, lds, S(stream_), a);
+        else if (levels) hipLaunchKernelGGL((kern::k_score16f<16, true, false, true>), grid, block, lds, S(stream_), a);
         else if (swar) hipLaunchKernelGGL((kern::k_score16f<16, true>), grid, block, lds, S(stream_), a);
         else if (framed) hipLaunchKernelGGL((kern::k_score16f<16>), grid, block, lds, S(stream_), a);
         else if (half) hipLaunchKernelGGL((kern::k_score16<16, true>), grid, block, lds, S(stream_), a);
@@ -1334,6 +1360,7 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
         break;
       default:
         if (unit) hipLaunchKernelGGL((kern::k_score16f<8, true, true>), grid, block, lds, S(stream_), a);
+        else if (levels) hipLaunchKernelGGL((kern::k_score16f<8, true, false, true>), grid, block, lds, S(stream_), a);
         else if (swar) hipLaunchKernelGGL((kern::k_score16f<8, true>), grid, block, lds, S(stream_), a);
         else if (framed) hipLaunchKernelGGL((kern::k_score16f<8>), grid, block, lds, S(stream_), a);
         else if (half) hipLaunchKernelGGL((kern::k_score16<8, true>), grid, block, lds, S(stream_), a);
@@ -1357,6 +1384,7 @@ void DeviceModule::ScoreLaunch(DevQuery *q, DevDb *d, uint64_t cand_begin, uint6
   times_.score_launches_unit += unit ? 1 : 0;
   times_.score_launches_pair += pairs ? 1 : 0;
   times_.score_launches_sparse += sparse ? 1 : 0;
+  times_.score_launches_levels += levels && (sparse || (packed && !unit && !pairs)) ? 1 : 0;
   P.active = true;
   P.guarded = half && guard;
   P.cand_begin = cand_begin;

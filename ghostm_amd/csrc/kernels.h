@@ -1462,6 +1462,9 @@ struct ScoreArgs {
   // k_score16f<S, true> over sparse segments (kScoreRowsSparse): the profile
   // slots per block and code rows per slot (0 = kScoreQmax, kProfRows16)
   uint32_t prof_slots, prof_rows;
+  // k_score16f<S, true, false, true> (restart levels): each END of a half
+  // restarts its frame swar_step above the last, up to swar_cap
+  uint32_t swar_step, swar_cap;
 };
 __device__ inline uint32_t ProfSlots(const ScoreArgs &a) { return a.prof_slots ? a.prof_slots : (uint32_t)kScoreQmax; }
 __device__ inline uint32_t ProfRows(const ScoreArgs &a) { return a.prof_rows ? a.prof_rows : kProfRows16; }
@@ -1617,6 +1620,11 @@ __device__ inline uint32_t PkSubI16(uint32_t a, uint32_t b) {
   asm("v_pk_sub_i16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
   return r;
 }
+__device__ inline uint32_t PkMinU16(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 __device__ inline uint32_t PkSign(uint32_t a) {  // 0xFFFF in each negative half
   uint32_t r;
   // op_sel_hi:[0,1]: the high lane takes the shift count from the constant's low
@@ -1739,7 +1747,9 @@ __device__ inline uint32_t MulU24(uint32_t a, uint32_t b) {
 // Codes 0..24 carry M + ext_pen as a two's-complement delta, END the absolute
 // restart value (read with m = 0 in the END column itself), every other code
 // and the padding rows a drop that leaves H - drop > 0 far below the frame.
-template <class C, bool FRAMED, bool SWAR = false>
+// END_DROP (restart levels): END reads the drop too; its column comes out as
+// the level through E, as in the UNIT kernel.
+template <class C, bool FRAMED, bool SWAR = false, bool END_DROP = false>
 __device__ __forceinline__ void BuildProfile16(const ScoreArgs &a, const ScoreTask &t, short *s_prof16,
                                                uint32_t RS) {
   const uint32_t nrows = ProfRows(a);  // code rows per slot: 32, or 27 (codes 0..26) for the sparse blocks
@@ -1750,7 +1760,7 @@ __device__ __forceinline__ void BuildProfile16(const ScoreArgs &a, const ScoreTa
     const uint32_t q = e >> 5, c = e & 31;
     int v = c < 25 ? a.mat[c * 32 + q] : 0;
     if constexpr (SWAR) {
-      s_enc[e] = (short)(c < kSeqEnd ? (uint32_t)(v + extp) & 0xFFFFu : c == kSeqEnd ? a.swar_restart : drop);
+      s_enc[e] = (short)(c < kSeqEnd ? (uint32_t)(v + extp) & 0xFFFFu : c == kSeqEnd && !END_DROP ? a.swar_restart : drop);
       continue;
     }
     if constexpr (FRAMED) v = c == kFillCode ? kNeg16 : v + extp;
@@ -1766,7 +1776,7 @@ __device__ __forceinline__ void BuildProfile16(const ScoreArgs &a, const ScoreTa
     if (r < a.pad) {
 #pragma unroll
       for (int k = 0; k < 16; ++k) w[k] = neg;
-      if constexpr (SWAR)  // END (code 25, the high half of word 12): the restart, as in real rows
+      if constexpr (SWAR && !END_DROP)  // END (code 25, the high half of word 12): the restart, as in real rows
         w[kSeqEnd >> 1] = (w[kSeqEnd >> 1] & 0xFFFFu) | (a.swar_restart << 16);
     } else {
       const uint32_t q = a.qseq[(size_t)(t.q_first + slot) * a.L + (r - a.pad)];
@@ -2047,10 +2057,25 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16(ScoreArgs a) {
 // 16-bit rows, so a block holds the profiles of at most kScoreQmaxUnit queries
 // (the host uses this kernel when a segment averages enough candidates per
 // query to fill its blocks).
-template <int S, bool SWAR = false, bool UNIT = false>
+//
+// LEVELS = true (with SWAR, not UNIT; round 6): restart levels instead of the
+// second END's reset. Each END of a half restarts its frame at that half's
+// level, swar_restart + k * swar_step for its k-th END in the window, above
+// every value before it (the host checks that the window's most ENDs fit below
+// the f16 infinity pattern, and caps the level at swar_cap: columns past a
+// window cut at the DB's end are all END and never read). As in the UNIT
+// kernel, the column before an END floors E at the level in that half and the
+// END row of the profile is the drop, so every row of the END column comes out
+// as the level (real 0) through E: no diagonal mask, and no wave-wide branch
+// that clears E when some half meets its second END, which at cfg2's
+// 75-residue subjects (two or three ENDs in every 163-column window) ran in
+// most columns.
+template <int S, bool SWAR = false, bool UNIT = false, bool LEVELS = false>
 __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
   GHOSTM_POISON_LDS();
   static_assert(!UNIT || SWAR, "unit-pair words carry integer patterns");
+  static_assert(!LEVELS || (SWAR && !UNIT), "restart levels: the 16-bit-row integer-pattern kernel");
+  constexpr bool LA = UNIT || LEVELS;  // E floored at the restart in the column before an END
   using C = Cells<true>;
   extern __shared__ __attribute__((aligned(16))) short s_prof16[];
   const ScoreTask t = a.tasks[blockIdx.x];
@@ -2062,7 +2087,7 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
   if constexpr (UNIT)
     BuildProfileUnit(a, t, reinterpret_cast<uint32_t *>(s_prof16), RS);
   else
-    BuildProfile16<C, true, SWAR>(a, t, s_prof16, RS);
+    BuildProfile16<C, true, SWAR, LEVELS>(a, t, s_prof16, RS);
   __syncthreads();
 
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -2125,6 +2150,9 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
   const uint32_t ONE = SWAR ? 0x00010001u : C::kOne;
   const uint32_t RESTART = a.swar_restart * 0x10001u;
   const uint32_t SWLOW = a.swar_low * 0x10001u;
+  // LEVELS: each half's restart level for its next END, one step up per END
+  const uint32_t STEP2 = LEVELS ? a.swar_step * 0x10001u : 0u, CAP2 = LEVELS ? a.swar_cap * 0x10001u : 0u;
+  uint32_t rlev = RESTART;
 
   // Frame bases: until the window's first true END the frame is based near
   // -2040 (sigma(j) = -2040 + (G + j) * ext_pen), so every value there is
@@ -2155,9 +2183,9 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
   // frame for H (sigma(-i - 1)), and a real F below 0
   uint32_t hout = sig_prev, fout = NEGF, hprev = sig_prev;
   uint32_t c0A = dbp[xA], c0B = dbp[xB], c1A = dbp[xA + 1], c1B = dbp[xB + 1];
-  const uint32_t steps = a.base + a.G - 1;
   const uint32_t wA_ = vA ? wA : 0u, wB_ = vB ? wB : 0u;
-  if constexpr (UNIT) {
+  const uint32_t steps = a.base + a.G - 1;
+  if constexpr (LA) {
     // lane 0 starts at column 0 (no fill column sets E's floor for it): E enters
     // as RESTART where that column is END, as after any column before an END
     if (i == 0) {
@@ -2213,7 +2241,11 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
     uint32_t sigc = sig;
     if constexpr (SWAR) {
       mreg = ONE;
-      if (any_end) {
+      if (any_end && LEVELS) {
+        // this half's level; the next END of the half restarts one step higher
+        sigc = BfiV(end, rlev, sig);
+        rlev = PkMinU16(rlev + (end & STEP2), CAP2);
+      } else if (any_end) {
         sigc = BfiV(end, RESTART, sig);
         mreg = ONE & ~end;
         const uint32_t reset = end & seen;
@@ -2243,7 +2275,7 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
     // the next column's frame: one step on, or (f16) restarted at 0 after a true END
     const uint32_t zn = SWAR ? sigc + EXTP : BfiV(end, EXTP, W(HF(sig) + HF(EXTP)));
     uint32_t zf = zn;  // E's floor: real 0 of the next column's frame
-    if constexpr (UNIT) {
+    if constexpr (LA) {
       // UNIT: where the NEXT column is END, E's floor is RESTART, so every row
       // of the END column enters with E = RESTART; its diagonal reads the
       // profile's drop (old H + drop < RESTART) and F stays below, so each row
@@ -2253,7 +2285,7 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
       if (__builtin_amdgcn_ballot_w64(max((uint16_t)c0A, (uint16_t)c0B) >= (uint16_t)kSeqEnd)) {
         uint32_t ne = PkSign(PkAddU16(c0A | (c0B << 16), 0x7FE77FE7u));
         if constexpr (in_fill) ne = (int)(step - i) + 1 < 0 ? 0u : ne;  // the next column is still a fill column
-        zf = BfiV(ne, RESTART, zn);
+        zf = BfiV(ne, LEVELS ? rlev : RESTART, zn);
       }
     }
     const hf2 Z1 = HF(zf);

@@ -85,6 +85,7 @@ class GhostmStats(ctypes.Structure):
         ("seed_compact_redo", c_uint64),
         ("score_launches_sparse", c_uint64),
         ("traceback_launches_keyframe", c_uint64),
+        ("score_launches_levels", c_uint64),
     ]
 
     def as_dict(self) -> dict:

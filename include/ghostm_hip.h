@@ -223,6 +223,8 @@ typedef struct GhostmStats {
   uint64_t score_launches_sparse;   /* K2 launches of sparse segments run by the 16-row profile kernel (k_score16f<16, true>,
                                        seven query profiles per block) */
   uint64_t traceback_launches_keyframe; /* K3 key DPs run with the column-framed E chain (k_traceback_key FRAME) */
+  uint64_t score_launches_levels;   /* K2 launches of the 16-bit-row integer-pattern kernel with restart levels
+                                       (k_score16f<S, true, false, true>) */
 } GhostmStats;
 
 /* Session: parse `aln` options exactly like the reference (getopt string

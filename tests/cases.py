@@ -82,6 +82,21 @@ DATASETS = {
         ("db", ["-i", "{golden}/testset_db.fasta", "-o", "{d}/db"]),
         ("qry", ["-i", "{d}/q.fa", "-o", "{d}/q", "-l", "127"]),
     ],
+    # subjects of 10-20 residues: every K2 window crosses up to 15 subject ENDs
+    # (the restart-level kernel's levels), and of 4-9 (more ENDs per window than
+    # the levels hold: the second-END reset kernel runs instead)
+    "syn_subj10": [
+        ("synth", ["-d", "{d}/db.fa", "-q", "{d}/q.fa", "-n", "300", "-N", "40000", "-s", "17",
+                   "-a", "60", "-b", "127", "-m", "10", "-x", "20"]),
+        ("db", ["-i", "{d}/db.fa", "-o", "{d}/db"]),
+        ("qry", ["-i", "{d}/q.fa", "-o", "{d}/q", "-l", "127"]),
+    ],
+    "syn_subj4": [
+        ("synth", ["-d", "{d}/db.fa", "-q", "{d}/q.fa", "-n", "300", "-N", "30000", "-s", "19",
+                   "-a", "60", "-b", "127", "-m", "4", "-x", "9"]),
+        ("db", ["-i", "{d}/db.fa", "-o", "{d}/db"]),
+        ("qry", ["-i", "{d}/q.fa", "-o", "{d}/q", "-l", "127"]),
+    ],
     # the same queries against a one-subject DB (DB::GetID's early return,
     # reference db.h:115-117, is the only branch taken)
     "cfg2_single": [
@@ -169,6 +184,9 @@ VARIANTS = [
     ("cfg2_20k", "default", [], {}),
     ("cfg2_20k", "y2", ["-y", "2"], {}),
     ("cfg2_single", "default", [], {}),
+    ("syn_subj10", "default", [], {}),
+    ("syn_subj10", "y2", ["-y", "2"], {}),
+    ("syn_subj4", "default", [], {}),
 ] + [
     # BASELINE configs[4]: -r 64, PAM250, -y 2 over the whole gap sweep
     # {8,10,11,14} x {1,2} (G11/E1 is syn_small/r64_pam250 above)

@@ -93,6 +93,37 @@ def test_gpu_sparse_rows_k2_matches_reference_golden(ds, var, opts, env, dataset
         assert st["score_launches_sparse"] == st["score_launches"]
 
 
+@pytest.mark.parametrize("form", ["default", "sparse", "swar16", "levels0", "sparse_levels0"])
+@pytest.mark.parametrize("ds,var,opts", [("syn_subj10", "default", []), ("syn_subj10", "y2", ["-y", "2"]),
+                                         ("syn_subj4", "default", []), ("protein_testset", "y0", []),
+                                         ("cfg2_single", "default", [])])
+def test_k2_restart_levels_match_golden(form, ds, var, opts, dataset, golden, tmp_path):
+    """K2's restart levels (k_score16f<S, true, false, true>: each END of a
+    window restarts one level higher, E floored at the level in the column
+    before, no second-END reset) on DBs whose windows cross many subject ENDs
+    (10-20-residue subjects: up to 15 per window), against the oracle; with
+    4-9-residue subjects the levels do not fit and the reset kernel runs
+    instead. GHOSTM_K2_LEVELS=0 forces the reset kernel everywhere. Against the
+    reference program's output (golden) and the oracle."""
+    d = dataset(ds)
+    env = {"sparse": {"GHOSTM_K2": "sparse"}, "swar16": {"GHOSTM_K2": "swar16"},
+           "levels0": {"GHOSTM_K2": "swar16", "GHOSTM_K2_LEVELS": "0"},
+           "sparse_levels0": {"GHOSTM_K2": "sparse", "GHOSTM_K2_LEVELS": "0"}}.get(form, {})
+    text, st = _gpu_text(d, opts, env, str(tmp_path / "g.out"))
+    (tmp_path / "g.out").write_bytes(text)
+    assert cases.sha256(str(tmp_path / "g.out")) == golden["aln"][f"{ds}/{var}"]["sha256"]
+    assert text == cases.run_aln(cases.ORACLE, d, opts, {}, str(tmp_path / "o.out"))
+    assert text.count(b"\n") > (50 if ds.startswith("syn_subj") else 0)
+    assert st["score_launches_swar"] == st["score_launches"] > 0
+    rows = st["score_launches"] - st["score_launches_unit"] - st["score_launches_pair"]
+    if form in ("levels0", "sparse_levels0") or ds == "syn_subj4":
+        assert st["score_launches_levels"] == 0
+    elif form != "default":  # the forced 16-bit-row kernels, with levels
+        assert st["score_launches_levels"] == rows == st["score_launches"]
+    else:
+        assert st["score_launches_levels"] == rows
+
+
 @pytest.mark.parametrize("merge", ["device", "device_thread", "host"])
 @pytest.mark.parametrize("ds,var,opts,env", cases.BATCH_VARIANTS,
                          ids=[f"{v[0]}/{v[1]}" for v in cases.BATCH_VARIANTS])
