@@ -2070,6 +2070,11 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16(ScoreArgs a) {
 // that clears E when some half meets its second END, which at cfg2's
 // 75-residue subjects (two or three ENDs in every 163-column window) ran in
 // most columns.
+// Untested columns of the look-ahead kernels take their END test from the
+// previous column's look-ahead (-DGHOSTM_K2_LAREUSE=0: their own, A/B).
+#ifndef GHOSTM_K2_LAREUSE
+#define GHOSTM_K2_LAREUSE 1
+#endif
 template <int S, bool SWAR = false, bool UNIT = false, bool LEVELS = false>
 __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
   GHOSTM_POISON_LDS();
@@ -2185,6 +2190,10 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
   uint32_t c0A = dbp[xA], c0B = dbp[xB], c1A = dbp[xA + 1], c1B = dbp[xB + 1];
   const uint32_t wA_ = vA ? wA : 0u, wB_ = vB ? wB : 0u;
   const uint32_t steps = a.base + a.G - 1;
+  // LA: the look-ahead's END test of the next column's codes, which that column
+  // reuses when it is untested (first: column 0's codes, for G = 1)
+  uint32_t la_ne = PkSign(PkAddU16(c0A | (c0B << 16), 0x7FE77FE7u));
+  bool la_any = __builtin_amdgcn_ballot_w64(la_ne != 0) != 0;
   if constexpr (LA) {
     // lane 0 starts at column 0 (no fill column sets E's floor for it): E enters
     // as RESTART where that column is END, as after any column before an END
@@ -2227,7 +2236,11 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
     // END mask is formed only when some lane meets END
     uint32_t end = 0;
     bool any_end;
-    if constexpr (SWAR && !tested) {
+    if constexpr (SWAR && !tested && LA && GHOSTM_K2_LAREUSE) {
+      // the previous column's look-ahead tested these codes already
+      any_end = la_any;
+      end = la_ne;
+    } else if constexpr (SWAR && !tested) {
       any_end = __builtin_amdgcn_ballot_w64(max((uint16_t)rA, (uint16_t)rB) >= (uint16_t)kSeqEnd) != 0;
       if (any_end) end = end_mask();
     } else {
@@ -2282,9 +2295,14 @@ __global__ __launch_bounds__(kScoreBlock) void k_score16f(ScoreArgs a) {
       // comes out as RESTART = real 0 of the restarted frame without masking
       // the old H. c0A/c0B hold the next column's codes (the END padding past a
       // window cut at the DB's end; the drain columns' values are never read).
-      if (__builtin_amdgcn_ballot_w64(max((uint16_t)c0A, (uint16_t)c0B) >= (uint16_t)kSeqEnd)) {
+      // (kept for the next column's END test when that column is untested: its
+      // codes are these, and no lane is in the fill there)
+      la_any = __builtin_amdgcn_ballot_w64(max((uint16_t)c0A, (uint16_t)c0B) >= (uint16_t)kSeqEnd) != 0;
+      la_ne = 0;
+      if (la_any) {
         uint32_t ne = PkSign(PkAddU16(c0A | (c0B << 16), 0x7FE77FE7u));
         if constexpr (in_fill) ne = (int)(step - i) + 1 < 0 ? 0u : ne;  // the next column is still a fill column
+        la_ne = ne;
         zf = BfiV(ne, LEVELS ? rlev : RESTART, zn);
       }
     }
