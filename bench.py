@@ -57,7 +57,7 @@ FULL_GOLDEN = os.path.join(REPO, "tests", "golden", "full_golden.json")
 VALU_ISSUE = os.path.join(REPO, "profiles", "r2_valu_issue.json")
 PMC = os.path.join(REPO, "profiles", "pmc_traffic.json")  # cfg4; other presets: pmc_traffic_<preset>.json
 ISA_MIX = os.path.join(REPO, "profiles", "r3_k2_isa_mix.json")  # k_score16f<32, true> (16-bit profile rows)
-ISA_MIX_UNIT = os.path.join(REPO, "profiles", "r3u_k2_isa_mix.json")  # k_score16f<32, true, true> (unit-pair words)
+ISA_MIX_UNIT = os.path.join(REPO, "profiles", "r6_k2_unit_isa_mix.json")  # k_score16f<32, true, true> (unit-pair words, round 6)
 ISA_MIX_PAIR = os.path.join(REPO, "profiles", "r5_k2_pair_isa_mix.json")  # k_score_pair<32> (pair table)
 VOP2_IN_MIX_CYCLES = 3.44  # fast VOP2 add inside a 1:2 pk_max3:add stream (profiles/r2c_valu_issue_pmc.txt)
 
